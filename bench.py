@@ -1,0 +1,191 @@
+"""Headline benchmark (BASELINE.json `metric`): train images/sec at batch 64 per GPU,
+36x2048 region features, seq_len 20, the 6+6-block d_model=512 h=8 Transformer (C2),
+bf16 MFMA path, synthetic data resident in HBM, random-init weights.
+
+One step = TRANSFORMER.train_step (forward + backward + [RCCL all-reduce] + Adam) over
+one 64-image batch per GPU.  N>1: launched by torch.distributed.run, one rank per GPU,
+weak scaling (64 images per rank), exact global-mean CE.
+
+Prints ONE JSON line (rank 0).  `roofline` is the whole train step on the MFMA roof
+(519.9157 GFLOP per 64-image step), plus the dominant GEMM timed alone;
+`cpu_baseline` times the CPU oracle (fp32 eager torch, train mode) on this host.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "image-caption_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "train images/sec @ batch=64, 36×2048 feats, seq_len=20; 1/2/4/8 MI355X"
+PEAK_BF16_TFLOPS = 2516.6          # 256 CU x 4096 FLOP/clk x 2.4 GHz (dense)
+GFLOP_PER_IMAGE = 8.12368          # SURVEY §8(d) closed form == torch.profiler count
+B, N, T = 64, 36, 20
+
+
+def step_flops_per_image(cfg, N, T):
+    """SURVEY §8(d) closed form: train = 3*fwd - 2BN(F+P)d (no dX for the feature embed)."""
+    d, f, V = cfg.encode_input_size, cfg.encode_hidden_size, cfg.num_vocab
+    F, P, L = cfg.encode_dim_features, cfg.encode_dim_positions, T - 1
+    Le, Ld = cfg.encode_num_blocks, cfg.decode_num_blocks
+    emb = 2 * N * (F + P) * d
+    fwd = (emb + Le * (N * (8 * d * d + 4 * d * f) + 4 * N * N * d) + 2 * L * d * d
+           + Ld * (L * (8 * d * d + 4 * d * f) + 4 * L * L * d + 4 * L * d * d + 4 * N * d * d + 4 * L * N * d)
+           + 2 * L * d * V)
+    return 3 * fwd - emb
+
+
+def dominant_gemm(eng, steps=50):
+    """Time the encoder FFN-up GEMM ([2304,512] x [512,2048]^T, bf16, the largest GEMM
+    class of the step) with HIP events on the launching stream."""
+    import ctypes as C
+    from capgen import _lib
+    lib = _lib.load()
+    M, Nn, K = B * N, 2048, 512
+    A = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    W = torch.randn(Nn, K, device="cuda", dtype=torch.bfloat16)
+    Cc = torch.empty(M, Nn, device="cuda", dtype=torch.bfloat16)
+    bias = torch.zeros(Nn, device="cuda")
+    s = torch.cuda.current_stream()
+
+    def launch():
+        _lib.check(lib.capgen_debug_gemm(M, Nn, K, C.c_void_p(A.data_ptr()), K, 0, C.c_void_p(W.data_ptr()), K, 0,
+                                         C.c_void_p(Cc.data_ptr()), Nn, 1, 1, C.c_void_p(bias.data_ptr()), 1.0, 0, 1,
+                                         C.c_void_p(s.cuda_stream)))
+    for _ in range(10):
+        launch()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(steps):
+        launch()
+    e1.record(s)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    flops = 2.0 * M * Nn * K
+    return {"kernel": "gemm_kernel<bf16,bf16,NT> enc FFN-up 2304x2048x512 (+bias,relu)",
+            "avg_us": round(ms * 1e3, 2), "achieved": round(flops / (ms * 1e-3) / 1e12, 1), "unit": "TFLOP/s",
+            "frac": round(flops / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4)}
+
+
+def cpu_baseline(cfg, steps=3, warmup=1):
+    """The pinned CPU oracle (fp32 eager torch, train mode = dropout on) on this host's cores:
+    a bounded sample of the same workload (same B/N/T/model), time per step -> images/s."""
+    sys.path.insert(0, REPO)
+    from oracle import capgen_oracle as O
+    from capgen.params import reference_init_state_dict
+    from capgen.synthetic import synthetic_batch
+    threads = torch.get_num_threads()
+    f, p, c = synthetic_batch(B, N, cfg.encode_dim_features, cfg.encode_dim_positions, T, cfg.num_vocab, seed=1000)
+    P = O.make_params(reference_init_state_dict(cfg.replace(dtype="fp32"), seed=0))
+    opt = O.make_adam(P, cfg)
+    for _ in range(warmup):
+        O.train_step(P, opt, cfg, f, p, c, training=True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        O.train_step(P, opt, cfg, f, p, c, training=True)
+    dt = (time.perf_counter() - t0) / steps
+    return {"value": round(B / dt, 2), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{warmup} warm-up + {steps} timed C2 train steps (B={B}, fp32 eager torch CPU, dropout on), "
+                      f"{dt:.3f} s/step"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    args = ap.parse_args()
+
+    from capgen import preset
+    from capgen.engine import Engine
+    from capgen.params import reference_init_state_dict
+    from capgen.synthetic import synthetic_batch
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = preset("C2", dtype=args.dtype, dropout=0.3)   # config.py:61 DROPOUT; attention 0.1
+    eng = Engine(cfg, dev)
+    eng.load_state_dict({k: torch.from_numpy(v) for k, v in reference_init_state_dict(cfg, seed=0).items()})
+    if args.no_graph:
+        eng.set_graph(False)
+    if world > 1:
+        from capgen.dp import init_engine_dp
+        init_engine_dp(eng, rank, world)
+
+    f, p, c = synthetic_batch(B, N, cfg.encode_dim_features, cfg.encode_dim_positions, T, cfg.num_vocab,
+                              seed=1000 + rank)
+    fdt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    f = f.to(dev, fdt).contiguous()
+    p = p.to(dev).contiguous()
+    c = c.to(dev).contiguous()
+    loss = torch.zeros(1, device=dev)
+    from capgen import _lib
+    ft = _lib.BF16 if fdt == torch.bfloat16 else _lib.F32
+
+    for _ in range(args.warmup):
+        eng.train_step_raw(f, ft, p, c, B, N, T, loss)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.train_step_raw(f, ft, p, c, B, N, T, loss)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    final_loss = loss.item()
+
+    images = B * world * args.steps
+    value = images / elapsed
+    ms = elapsed / args.steps * 1e3
+    gfl_img = step_flops_per_image(cfg, N, T) / 1e9
+    achieved = value * gfl_img / 1e3 / world  # TFLOP/s per GPU
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (region feats/positions/captions, SURVEY §8(d))",
+        "config": {"workload": "C2 train step: B=64/GPU, N=36 regions x F=2048, P=84, T=20, 6+6 blocks d=512 h=8 "
+                               "f=2048, V=10000, dropout 0.3/0.1, Adam lr 5e-4",
+                   "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}"},
+        "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / PEAK_BF16_TFLOPS, 5), "traffic": None,
+                     "scope": f"whole train step, {gfl_img:.5f} GFLOP/image algorithmic (SURVEY §8(d))"},
+        "final_loss": round(final_loss, 5),
+    }
+    if rank == 0 and world == 1:
+        out["dominant_kernel"] = dominant_gemm(eng)
+        if not args.no_cpu_baseline:
+            del eng
+            torch.cuda.empty_cache()
+            out["cpu_baseline"] = cpu_baseline(cfg, steps=args.cpu_steps)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,131 @@
+"""ctypes binding of libcapgen.so (the C ABI declared in include/capgen.h).
+
+The library is loaded AFTER `import torch`, so its NEEDED libamdhip64.so.7 resolves to
+the HIP runtime torch already mapped: device pointers, streams and events are shared
+with PyTorch.  There is no fallback: if the library is missing, importing the engine
+raises, loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must precede the dlopen, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcapgen.so")
+ABI_VERSION = 1
+
+F32, BF16 = 0, 1
+
+
+class capgen_config(C.Structure):
+    _fields_ = [
+        ("num_vocab", C.c_int32), ("max_length", C.c_int32),
+        ("dim_features", C.c_int32), ("dim_positions", C.c_int32),
+        ("enc_d", C.c_int32), ("enc_ff", C.c_int32), ("enc_blocks", C.c_int32), ("enc_heads", C.c_int32),
+        ("dim_word_embedding", C.c_int32),
+        ("dec_d", C.c_int32), ("dec_ff", C.c_int32), ("dec_blocks", C.c_int32), ("dec_heads", C.c_int32),
+        ("dropout", C.c_float), ("attention_dropout", C.c_float),
+        ("pad_idx", C.c_int32), ("encode_mask", C.c_int32), ("focal_loss", C.c_int32),
+        ("dtype", C.c_int32), ("max_batch", C.c_int32), ("max_regions", C.c_int32),
+        ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float),
+        ("seed", C.c_uint64),
+    ]
+
+
+class capgen_param_info(C.Structure):
+    _fields_ = [("name", C.c_char * 96), ("ndim", C.c_int32), ("rows", C.c_int64), ("cols", C.c_int64),
+                ("offset", C.c_int64), ("row_stride", C.c_int64)]
+
+
+_P = C.c_void_p
+_SIGS = {
+    "capgen_last_error": (C.c_char_p, []),
+    "capgen_abi_version": (C.c_int, []),
+    "capgen_param_table": (C.c_int, [C.POINTER(capgen_config), C.POINTER(capgen_param_info), C.c_int,
+                                     C.POINTER(C.c_int), C.POINTER(C.c_int64)]),
+    "capgen_create": (C.c_int, [C.POINTER(capgen_config), C.c_int, C.POINTER(_P)]),
+    "capgen_destroy": (C.c_int, [_P]),
+    "capgen_get_params": (C.c_int, [_P, _P, C.c_int64]),
+    "capgen_set_params": (C.c_int, [_P, _P, C.c_int64]),
+    "capgen_get_grads": (C.c_int, [_P, _P, C.c_int64]),
+    "capgen_get_adam_state": (C.c_int, [_P, C.POINTER(C.c_int64), _P, _P, C.c_int64]),
+    "capgen_set_adam_state": (C.c_int, [_P, C.c_int64, _P, _P, C.c_int64]),
+    "capgen_arenas": (C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), C.POINTER(C.c_int64)]),
+    "capgen_set_training": (C.c_int, [_P, C.c_int]),
+    "capgen_set_graph": (C.c_int, [_P, C.c_int]),
+    "capgen_forward": (C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int, _P, _P]),
+    "capgen_backward": (C.c_int, [_P, _P]),
+    "capgen_adam_step": (C.c_int, [_P, _P]),
+    "capgen_train_step": (C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int, _P, _P]),
+    "capgen_compute_loss": (C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int, _P, _P]),
+    "capgen_copy_logits": (C.c_int, [_P, _P, C.c_int64, _P]),
+    "capgen_greedy": (C.c_int, [_P, _P, C.c_int, _P, C.c_int, C.c_int, _P, _P, _P]),
+    "capgen_beam": (C.c_int, [_P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int, _P, _P]),
+    "capgen_set_rng_seed": (C.c_int, [_P, C.c_uint64]),
+    "capgen_debug_gemm": (C.c_int, [C.c_int, C.c_int, C.c_int, _P, C.c_int64, C.c_int, _P, C.c_int64, C.c_int,
+                                    _P, C.c_int64, C.c_int, C.c_int, _P, C.c_float, C.c_int, C.c_int, _P]),
+    "capgen_dp_unique_id": (C.c_int, [C.c_char_p]),
+    "capgen_dp_init": (C.c_int, [_P, C.c_char_p, C.c_int, C.c_int]),
+    "capgen_dp_set_global_count": (C.c_int, [_P, C.c_float]),
+}
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+
+
+def load():
+    """dlopen libcapgen.so once; raises if it was not built (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"capgen: {LIB_PATH} is missing — build it with "
+                          "`python -c 'import __graft_entry__ as g; g.build()'` (make -C image-caption_amd/csrc)")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.capgen_abi_version() != ABI_VERSION:
+        raise ImportError("capgen: libcapgen.so ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        raise RuntimeError("capgen: " + load().capgen_last_error().decode(errors="replace"))
+
+
+def to_c_config(cfg) -> capgen_config:
+    cfg.check_supported()
+    c = capgen_config()
+    c.num_vocab, c.max_length = cfg.num_vocab, cfg.max_length
+    c.dim_features, c.dim_positions = cfg.encode_dim_features, cfg.encode_dim_positions
+    c.enc_d, c.enc_ff = cfg.encode_input_size, cfg.encode_hidden_size
+    c.enc_blocks, c.enc_heads = cfg.encode_num_blocks, cfg.encode_num_heads
+    c.dim_word_embedding = cfg.dim_word_embedding
+    c.dec_d, c.dec_ff = cfg.decode_input_size, cfg.decode_hidden_size
+    c.dec_blocks, c.dec_heads = cfg.decode_num_blocks, cfg.decode_num_heads
+    c.dropout, c.attention_dropout = cfg.dropout, cfg.attention_dropout
+    c.pad_idx, c.encode_mask, c.focal_loss = cfg.pad_idx, int(cfg.encode_mask), int(cfg.focal_loss)
+    c.dtype = F32 if cfg.dtype == "fp32" else BF16
+    c.max_batch, c.max_regions = cfg.max_batch, cfg.max_regions
+    c.lr, c.beta1, c.beta2, c.eps = cfg.learning_rate, cfg.beta1, cfg.beta2, cfg.eps
+    c.seed = cfg.seed & 0xFFFFFFFFFFFFFFFF
+    return c
+
+
+def param_table(cfg):
+    """[(name, ndim, rows, cols, offset, row_stride)], arena_elems — host-only, no GPU needed."""
+    lib = load()
+    c = to_c_config(cfg)
+    n = C.c_int(0)
+    total = C.c_int64(0)
+    check(lib.capgen_param_table(C.byref(c), None, 0, C.byref(n), C.byref(total)))
+    arr = (capgen_param_info * n.value)()
+    check(lib.capgen_param_table(C.byref(c), arr, n.value, C.byref(n), C.byref(total)))
+    out = [(p.name.decode(), p.ndim, p.rows, p.cols, p.offset, p.row_stride) for p in arr]
+    return out, total.value

@@ -1,0 +1,213 @@
+"""Python handle over one libcapgen engine (one process, one device).
+
+Thin: argument checking, dtype/layout normalisation of torch tensors, the
+state_dict <-> packed-arena mapping, and current-stream plumbing.  All compute is in
+libcapgen.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import CapgenConfig
+from .params import PE_BUFFER, sinusoid_table
+
+
+def _ptr(t: torch.Tensor | None):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _stream(device) -> C.c_void_p:
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class Engine:
+    def __init__(self, cfg: CapgenConfig, device="cuda:0"):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("capgen: the engine runs on a HIP device (cuda:N under ROCm)")
+        self.lib = _lib.load()
+        self._c = _lib.to_c_config(cfg)
+        self.table, self.arena_elems = _lib.param_table(cfg)
+        h = C.c_void_p()
+        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self.device = torch.device("cuda", idx)
+        _lib.check(self.lib.capgen_create(C.byref(self._c), idx, C.byref(h)))
+        self.h = h
+        self.training = True
+        self._loss = torch.zeros(1, dtype=torch.float32, device=self.device)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.capgen_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- module state -------------------------------------------------------------------
+    def set_training(self, training: bool):
+        self.training = bool(training)
+        _lib.check(self.lib.capgen_set_training(self.h, int(self.training)))
+
+    def set_graph(self, enable: bool):
+        _lib.check(self.lib.capgen_set_graph(self.h, int(enable)))
+
+    def _arena_to_host(self, fn) -> np.ndarray:
+        buf = np.empty(self.arena_elems, dtype=np.float32)
+        _lib.check(fn(self.h, buf.ctypes.data_as(C.c_void_p), self.arena_elems))
+        return buf
+
+    def _unpack(self, arena: np.ndarray) -> "OrderedDict[str, torch.Tensor]":
+        sd = OrderedDict()
+        for name, ndim, rows, cols, off, stride in self.table:
+            view = np.lib.stride_tricks.as_strided(arena[off:], shape=(rows, cols), strides=(stride * 4, 4))
+            a = np.array(view, dtype=np.float32)
+            sd[name] = torch.from_numpy(a if ndim == 2 else a.reshape(cols))
+        return sd
+
+    def state_dict(self, with_buffer: bool = True):
+        """Reference-named f32 CPU tensors (checkpoint-compatible with model.py's keys)."""
+        torch.cuda.current_stream(self.device).synchronize()
+        sd = self._unpack(self._arena_to_host(self.lib.capgen_get_params))
+        if with_buffer:
+            sd[PE_BUFFER] = torch.from_numpy(sinusoid_table(self.cfg.max_length - 1, self.cfg.decode_input_size)[None])
+        return sd
+
+    def grads_state_dict(self):
+        torch.cuda.current_stream(self.device).synchronize()
+        return self._unpack(self._arena_to_host(self.lib.capgen_get_grads))
+
+    def load_state_dict(self, sd, strict: bool = True):
+        arena = np.zeros(self.arena_elems, dtype=np.float32)
+        seen = set()
+        for name, ndim, rows, cols, off, stride in self.table:
+            if name not in sd:
+                if strict:
+                    raise KeyError(f"capgen: missing key {name!r} in state_dict")
+                continue
+            v = sd[name]
+            v = v.detach().cpu().float().numpy() if isinstance(v, torch.Tensor) else np.asarray(v, np.float32)
+            want = (rows, cols) if ndim == 2 else (cols,)
+            if tuple(v.shape) != want:
+                raise ValueError(f"capgen: {name}: shape {tuple(v.shape)} != {want}")
+            view = np.lib.stride_tricks.as_strided(arena[off:], shape=(rows, cols), strides=(stride * 4, 4))
+            view[...] = v.reshape(rows, cols)
+            seen.add(name)
+        if strict:
+            extra = set(sd) - seen - {PE_BUFFER}
+            if extra:
+                raise KeyError(f"capgen: unexpected keys in state_dict: {sorted(extra)[:5]}")
+        torch.cuda.current_stream(self.device).synchronize()
+        _lib.check(self.lib.capgen_set_params(self.h, arena.ctypes.data_as(C.c_void_p), self.arena_elems))
+
+    def adam_state(self):
+        step = C.c_int64(0)
+        m = np.empty(self.arena_elems, np.float32)
+        v = np.empty(self.arena_elems, np.float32)
+        _lib.check(self.lib.capgen_get_adam_state(self.h, C.byref(step), m.ctypes.data_as(C.c_void_p),
+                                                  v.ctypes.data_as(C.c_void_p), self.arena_elems))
+        return step.value, self._unpack(m), self._unpack(v)
+
+    # ---- inputs ----------------------------------------------------------------------
+    def _inputs(self, feats, pos, caps=None):
+        dev = self.device
+        if feats.dtype not in (torch.float32, torch.bfloat16):
+            feats = feats.float()
+        feats = feats.to(dev, non_blocking=True).contiguous()
+        pos = pos.to(dev, dtype=torch.float32, non_blocking=True).contiguous()
+        if feats.dim() != 3 or pos.dim() != 3 or feats.shape[:2] != pos.shape[:2]:
+            raise ValueError("capgen: object_features [B,N,F] and position_features [B,N,P] must agree")
+        if feats.shape[2] != self.cfg.encode_dim_features or pos.shape[2] != self.cfg.encode_dim_positions:
+            raise ValueError("capgen: feature widths do not match the config")
+        ft = _lib.BF16 if feats.dtype == torch.bfloat16 else _lib.F32
+        if caps is not None:
+            caps = caps.to(dev, dtype=torch.int32, non_blocking=True).contiguous()
+            if caps.dim() != 2 or caps.shape[0] != feats.shape[0]:  # model.py:203
+                raise ValueError("capgen: target_caption must be [B, T] with the batch of the features")
+        return feats, ft, pos, caps
+
+    # ---- hot path --------------------------------------------------------------------
+    def forward(self, feats, pos, caps, loss_out=None):
+        f, ft, p, c = self._inputs(feats, pos, caps)
+        B, N, _ = f.shape
+        out = self._loss if loss_out is None else loss_out
+        _lib.check(self.lib.capgen_forward(self.h, _ptr(f), ft, _ptr(p), _ptr(c), B, N, c.shape[1], _ptr(out),
+                                           _stream(self.device)))
+        return out
+
+    def backward(self):
+        _lib.check(self.lib.capgen_backward(self.h, _stream(self.device)))
+
+    def adam_step(self):
+        _lib.check(self.lib.capgen_adam_step(self.h, _stream(self.device)))
+
+    def train_step(self, feats, pos, caps, loss_out=None):
+        f, ft, p, c = self._inputs(feats, pos, caps)
+        B, N, _ = f.shape
+        out = self._loss if loss_out is None else loss_out
+        _lib.check(self.lib.capgen_train_step(self.h, _ptr(f), ft, _ptr(p), _ptr(c), B, N, c.shape[1], _ptr(out),
+                                              _stream(self.device)))
+        return out
+
+    def train_step_raw(self, f, ft, p, c, B, N, T, out):
+        """Pre-normalised device tensors (bench loop): no checks, no copies."""
+        _lib.check(self.lib.capgen_train_step(self.h, _ptr(f), ft, _ptr(p), _ptr(c), B, N, T, _ptr(out),
+                                              _stream(self.device)))
+
+    def compute_loss(self, feats, pos, caps):
+        out = torch.zeros(1, dtype=torch.float32, device=self.device)
+        f, ft, p, c = self._inputs(feats, pos, caps)
+        B, N, _ = f.shape
+        _lib.check(self.lib.capgen_compute_loss(self.h, _ptr(f), ft, _ptr(p), _ptr(c), B, N, c.shape[1], _ptr(out),
+                                                _stream(self.device)))
+        return out
+
+    def logits(self, B, T):
+        out = torch.empty(B * (T - 1), self.cfg.num_vocab, dtype=torch.float32, device=self.device)
+        _lib.check(self.lib.capgen_copy_logits(self.h, _ptr(out), out.numel(), _stream(self.device)))
+        return out.view(B, T - 1, -1)
+
+    def greedy(self, feats, pos, want_attention=True):
+        f, ft, p, _ = self._inputs(feats, pos)
+        B, N, _ = f.shape
+        T = self.cfg.max_length
+        ids = torch.empty(B, T + 1, dtype=torch.int64, device=self.device)
+        attn = torch.empty(T - 1, B, N, dtype=torch.float32, device=self.device) if want_attention else None
+        _lib.check(self.lib.capgen_greedy(self.h, _ptr(f), ft, _ptr(p), B, N, _ptr(ids), _ptr(attn),
+                                          _stream(self.device)))
+        return ids, attn
+
+    def beam(self, feats, pos, beam_size):
+        f, ft, p, _ = self._inputs(feats, pos)
+        B, N, _ = f.shape
+        ids = torch.empty(B, self.cfg.max_length, dtype=torch.int64, device=self.device)
+        _lib.check(self.lib.capgen_beam(self.h, _ptr(f), ft, _ptr(p), B, N, int(beam_size), _ptr(ids),
+                                        _stream(self.device)))
+        return ids
+
+    def set_rng_seed(self, seed: int):
+        _lib.check(self.lib.capgen_set_rng_seed(self.h, seed & 0xFFFFFFFFFFFFFFFF))
+
+    # ---- data parallel -----------------------------------------------------------------
+    @staticmethod
+    def dp_unique_id() -> bytes:
+        lib = _lib.load()
+        buf = C.create_string_buffer(128)
+        _lib.check(lib.capgen_dp_unique_id(buf))
+        return buf.raw
+
+    def dp_init(self, uid: bytes, rank: int, world: int):
+        assert len(uid) == 128
+        _lib.check(self.lib.capgen_dp_init(self.h, uid, rank, world))
+
+    def dp_set_global_count(self, count: float):
+        _lib.check(self.lib.capgen_dp_set_global_count(self.h, float(count)))

@@ -1,0 +1,89 @@
+"""`TRANSFORMER` — drop-in for core/models.py:18-135 (the object `main.py` drives).
+
+main.py uses exactly: train_step, compute_loss, generate_caption, decode_captions, save,
+load (main.py:65,70,73,85,112,116,124,151).  Inputs arrive as host tensors; the wrapper
+stages them into persistent device buffers so the captured train-step hipGraph replays
+with fixed pointers (the reference did a synchronous pageable `.to(DEVICE)` per step,
+models.py:120-122).
+"""
+from __future__ import annotations
+
+import torch
+
+from .config import CapgenConfig
+from .model import Transformer
+from .utils import decode_captions, load_word_to_idx
+
+
+class MODEL_init:
+    def __init__(self, word_to_idx=None, word_to_idx_path=None):
+        if word_to_idx is None:
+            if word_to_idx_path is None:
+                raise ValueError("capgen: pass word_to_idx or word_to_idx_path (models.py:22)")
+            word_to_idx = load_word_to_idx(word_to_idx_path)
+        self.num_vocab = len(word_to_idx)
+        self.idx_to_word = {i: w for w, i in word_to_idx.items()}
+        self.model = None
+
+    def train_step(self, *a, **k):
+        raise NotImplementedError
+
+    def compute_loss(self, *a, **k):
+        raise NotImplementedError
+
+    def generate_caption(self, object_features, position_features, beam_size=None):
+        """models.py:34-56: None/1 -> greedy (+attention_list); int > 1 -> beam search."""
+        if beam_size in [None, 1]:
+            ids, attention_list = self.model.generate_caption_vector(object_features=object_features,
+                                                                     position_features=position_features)
+            return self.decode_captions(ids.cpu().numpy()), attention_list
+        if isinstance(beam_size, int) and beam_size > 1:
+            ids = self.model.beam_search(object_features=object_features, position_features=position_features,
+                                         beam_size=beam_size)
+            return self.decode_captions(ids.cpu().numpy()), None
+        assert isinstance(beam_size, int)
+        assert beam_size > 1 or beam_size in [None, 1]
+
+    def decode_captions(self, caption_vector):
+        return decode_captions(caption_vector, self.idx_to_word)
+
+    def save(self, path):
+        torch.save(self.model.state_dict(), path)
+
+    def load(self, path):
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        self.model.load_state_dict(sd)
+        self.model.eval()
+
+
+class TRANSFORMER(MODEL_init):
+    def __init__(self, config: CapgenConfig | None = None, word_to_idx=None, word_to_idx_path=None,
+                 device="cuda:0", state_dict=None):
+        super().__init__(word_to_idx, word_to_idx_path)
+        cfg = (config or CapgenConfig()).replace(num_vocab=self.num_vocab)
+        self.config = cfg
+        self.device = torch.device(device)
+        self.model = Transformer.from_config(cfg, self.device, state_dict=state_dict)
+        self._stage = {}
+
+    def _staged(self, name, t, dtype):
+        buf = self._stage.get(name)
+        if buf is None or buf.shape != t.shape or buf.dtype != dtype:
+            buf = torch.empty(t.shape, dtype=dtype, device=self.device)
+            self._stage[name] = buf
+        buf.copy_(t, non_blocking=True)
+        return buf
+
+    def train_step(self, batch_features, batch_positions, batch_captions):
+        """models.py:115-126: zero_grad + forward + backward + Adam, one engine call."""
+        fdt = torch.bfloat16 if self.config.dtype == "bf16" else torch.float32
+        f = self._staged("f", batch_features, fdt)
+        p = self._staged("p", batch_positions, torch.float32)
+        c = self._staged("c", batch_captions, torch.int32)
+        self.model.engine.train_step(f, p, c)
+
+    def compute_loss(self, object_features, position_features, target_caption):
+        """models.py:128-135 (no_grad; dropout follows train/eval state)."""
+        with torch.no_grad():
+            return self.model(object_features=object_features, position_features=position_features,
+                              target_caption=target_caption)

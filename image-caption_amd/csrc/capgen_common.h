@@ -1,0 +1,115 @@
+// capgen — shared device/host helpers for the gfx950 (MI355X, CDNA4) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+typedef __bf16 bf16;
+
+#define CAPGEN_HIP(expr)                                                                  \
+  do {                                                                                    \
+    hipError_t _e = (expr);                                                               \
+    if (_e != hipSuccess)                                                                 \
+      throw capgen::Error(std::string(#expr) + ": " + hipGetErrorString(_e) + " at " +    \
+                          __FILE__ + ":" + std::to_string(__LINE__));                     \
+  } while (0)
+
+namespace capgen {
+
+struct Error {
+  std::string msg;
+  explicit Error(std::string m) : msg(std::move(m)) {}
+};
+
+inline void require(bool ok, const std::string& what) {
+  if (!ok) throw Error(what);
+}
+
+// ---- scalar conversions -------------------------------------------------------------
+__device__ __forceinline__ float to_f(float x) { return x; }
+__device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f(float x);
+template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
+
+// 16-byte vector of T: 4 floats or 8 bf16.
+template <typename T> struct Vec16;
+template <> struct Vec16<float> {
+  static constexpr int N = 4;
+  typedef float4 type;
+};
+template <> struct Vec16<bf16> {
+  static constexpr int N = 8;
+  typedef uint4 type;
+};
+
+// Load/store `n` (=N per lane chunk) consecutive elements as f32.
+template <typename T, int N>
+__device__ __forceinline__ void load_f(const T* p, float (&out)[N]) {
+  if constexpr (sizeof(T) * N == 16) {
+    typedef typename Vec16<T>::type V;
+    V v = *reinterpret_cast<const V*>(p);
+    const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = to_f(e[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = to_f(p[i]);
+  }
+}
+template <typename T, int N>
+__device__ __forceinline__ void store_f(T* p, const float (&in)[N]) {
+  if constexpr (sizeof(T) * N == 16) {
+    typedef typename Vec16<T>::type V;
+    V v;
+    T* e = reinterpret_cast<T*>(&v);
+#pragma unroll
+    for (int i = 0; i < N; ++i) e[i] = from_f<T>(in[i]);
+    *reinterpret_cast<V*>(p) = v;
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) p[i] = from_f<T>(in[i]);
+  }
+}
+
+// ---- wave64 reductions (DPP/permute via __shfl_xor) ----------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---- counter-based dropout RNG --------------------------------------------------------
+// keep(seed, site, idx): a splitmix64-style finaliser of (seed, site, idx).  Masks are
+// regenerated bit-identically in the backward pass, so nothing is stored.
+__device__ __forceinline__ uint32_t mix32(uint64_t seed, uint32_t site, uint32_t idx) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (((uint64_t)site << 32) | idx) + 0x632BE59BD9B4E019ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= (z >> 31);
+  return (uint32_t)(z >> 32);
+}
+// true = keep.  p in [0,1).  threshold = p * 2^32.
+__device__ __forceinline__ bool drop_keep(uint64_t seed, uint32_t site, uint32_t idx, uint32_t thresh) {
+  return mix32(seed, site, idx) >= thresh;
+}
+inline uint32_t drop_threshold(float p) {
+  double t = (double)p * 4294967296.0;
+  return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+}
+
+// Dropout descriptor passed by value to kernels.  `seed_ptr` points at the device-side
+// step seed so a captured hipGraph replays with a fresh mask each step.
+struct Drop {
+  const uint64_t* seed_ptr;  // null => dropout off
+  uint32_t site;
+  uint32_t thresh;
+  float scale;  // 1/(1-p)
+};
+
+}  // namespace capgen

@@ -1,0 +1,1222 @@
+// capgen — the training/decoding engine behind the C ABI (include/capgen.h).
+//
+// One engine = one (process, device).  It owns the packed f32 parameter arena (+ bf16
+// shadow for the MFMA path), the gradient arena, Adam moments and every activation
+// buffer, and sequences the hot path as explicit forward/backward kernel launches on
+// its own HIP stream — no autograd, no tracing compiler.  A train step is captured once
+// per (shape, input pointers) into a hipGraph and replayed.
+//
+// Reference call stack restated: models.py:115-126 train_step ->
+// model.py:79-98 forward -> Encoder (model.py:294-332) -> EncoderBlock (modules.py:146-157)
+// -> Decoder (model.py:419-459) -> DecoderBlock (modules.py:185-206) -> classifier + CE
+// (model.py:93-96) -> autograd backward -> Adam.step.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "../../include/capgen.h"
+#include "attention.h"
+#include "gemm.h"
+#include "layout.h"
+#include "ops.h"
+
+using namespace capgen;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+#define NCCL_CHECK(expr)                                                                             \
+  do {                                                                                               \
+    ncclResult_t _r = (expr);                                                                        \
+    if (_r != ncclSuccess) throw Error(std::string(#expr) + ": " + ncclGetErrorString(_r));          \
+  } while (0)
+
+// bump allocator: a dry run (base == nullptr) sizes the block, the second run assigns pointers
+struct Planner {
+  char* base = nullptr;
+  size_t used = 0;
+  void* raw(size_t bytes) {
+    size_t off = (used + 255) & ~size_t(255);
+    used = off + bytes;
+    return base ? base + off : nullptr;
+  }
+  template <class P>
+  void take(P*& p, size_t count) {
+    p = (P*)raw(count * sizeof(P));
+  }
+};
+
+struct EncAct {
+  void *qkv, *att, *v1, *Y, *H, *v2;
+  float *P, *m1, *r1, *m2, *r2;
+};
+struct DecAct {
+  void *qkv, *atts, *vs, *D1, *qc, *attc, *vc, *D2, *H, *vf;
+  float *Ps, *ms, *rs, *Pc, *mc, *rc, *mf, *rf;
+};
+
+struct Acts {
+  int B = 0, N = 0, T = 0;  // capacity
+  // encoder
+  void* Aenc;
+  uint8_t* valid;
+  void* ev0;
+  float *em0, *er0;
+  std::vector<void*> X;
+  std::vector<EncAct> enc;
+  void* KV;
+  // decoder
+  int32_t *ids, *tgt;
+  float* count;
+  void* E;
+  void* dv0;
+  float *dm0, *dr0;
+  std::vector<void*> D;
+  std::vector<DecAct> dec;
+  float* logits;
+  void* dlogits;
+  float *loss_row, *grad_scale, *loss;
+  // scratch / backward
+  void *tmp, *gOut, *gRes, *gA, *gQKV, *gATT, *gH, *gQc, *gKV, *gE;
+};
+
+struct GenWS {
+  int R = 0, N = 0;  // capacity (rows, regions)
+  void *x, *x1, *x2, *q, *att, *tmp, *h, *E;
+  float *mean, *rstd, *Pc, *logits, *probs;
+  void *cache, *cache2;  // [Ld][R][Tcap][2d]
+  int32_t *ids, *ids2;   // [R][Tcap]
+  int64_t *seq, *seq2;   // beam [R][Tw]
+  float *bprob, *bprob2;
+  int32_t *bsrc, *btok;
+};
+
+__global__ void init_gen_ids_kernel(int64_t* out, int rows, int width, int32_t* ids, int tcap) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < rows * width) out[c] = (c % width) == 0 ? 1 : 0;
+  if (c < rows * tcap) ids[c] = (c % tcap) == 0 ? 1 : 0;
+}
+
+// one workgroup per image: top-k (descending, lowest index first on ties) over the k*V
+// candidates probs[j*B+i][v] + prob[j][i]   (model.py:183-190)
+__global__ void __launch_bounds__(256) beam_topk_kernel(const float* __restrict__ probs, const float* __restrict__ prev,
+                                                        int k_in, int B, int V, int k, float* __restrict__ out_prob,
+                                                        int32_t* __restrict__ out_src, int32_t* __restrict__ out_tok) {
+  __shared__ float bv[4];
+  __shared__ int bi[4];
+  __shared__ int chosen[16];
+  const int i = blockIdx.x;
+  const int total = k_in * V;
+  for (int sel = 0; sel < k; ++sel) {
+    float best = -INFINITY;
+    int bidx = 0x7fffffff;
+    for (int c = threadIdx.x; c < total; c += 256) {
+      bool used = false;
+      for (int u = 0; u < sel; ++u) used |= (chosen[u] == c);
+      if (used) continue;
+      const int j = c / V, v = c % V;
+      const float x = probs[((int64_t)j * B + i) * V + v] + (prev ? prev[j * B + i] : 0.f);
+      if (x > best || (x == best && c < bidx)) {
+        best = x;
+        bidx = c;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      float ov = __shfl_xor(best, o, 64);
+      int oi = __shfl_xor(bidx, o, 64);
+      if (ov > best || (ov == best && oi < bidx)) {
+        best = ov;
+        bidx = oi;
+      }
+    }
+    if ((threadIdx.x & 63) == 0) {
+      bv[threadIdx.x >> 6] = best;
+      bi[threadIdx.x >> 6] = bidx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      best = bv[0];
+      bidx = bi[0];
+      for (int w = 1; w < 4; ++w)
+        if (bv[w] > best || (bv[w] == best && bi[w] < bidx)) {
+          best = bv[w];
+          bidx = bi[w];
+        }
+      chosen[sel] = bidx;
+      out_prob[sel * B + i] = best;
+      out_src[sel * B + i] = bidx / V;
+      out_tok[sel * B + i] = bidx % V;
+    }
+    __syncthreads();
+  }
+}
+
+// dst row r = (j, i) <- src row (src[j][i], i); then optionally set column `col` to tok
+template <typename E>
+__global__ void beam_gather_kernel(const E* __restrict__ src, E* __restrict__ dst, int64_t row_elems,
+                                   int64_t copy_elems, const int32_t* __restrict__ bsrc, int B, int R,
+                                   const int32_t* __restrict__ tok, int col) {
+  const int r = blockIdx.y;
+  const int srow = bsrc[r] * B + (r % B);
+  const E* s = src + (int64_t)srow * row_elems;
+  E* d = dst + (int64_t)r * row_elems;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < copy_elems; c += (int64_t)gridDim.x * blockDim.x)
+    d[c] = (tok && c == col) ? (E)tok[r] : s[c];
+}
+
+}  // namespace
+
+struct capgen_engine {
+  capgen_config cfg;
+  Layout L;
+  int device = 0;
+  DType act = DType::BF16;
+  hipStream_t es = nullptr;  // engine stream
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  float *params = nullptr, *grads = nullptr, *am = nullptr, *av = nullptr;
+  bf16* shadow = nullptr;
+  float* pe = nullptr;  // [max_length-1, dd] f32 sinusoid table
+  int64_t* step = nullptr;
+  float* adam_scal = nullptr;
+  uint64_t* seed = nullptr;
+  float* scalars = nullptr;  // internal loss
+  bool training = true;
+  bool fwd_drop = true;  // dropout state of the last forward (backward must match)
+  int fB = 0, fN = 0, fT = 0;  // shape of the last forward
+  Acts a;
+  void* ws = nullptr;
+  GenWS g;
+  void* gws = nullptr;
+  // graph
+  bool graph_on = true;
+  hipGraphExec_t gexec = nullptr;
+  struct Key {
+    const void *f, *p, *c;
+    float* loss;
+    int ft, B, N, T;
+    bool drop;
+    bool operator==(const Key& o) const {
+      return f == o.f && p == o.p && c == o.c && loss == o.loss && ft == o.ft && B == o.B && N == o.N && T == o.T &&
+             drop == o.drop;
+    }
+  } gkey{};
+  // data parallel
+  ncclComm_t comm = nullptr;
+  int rank = 0, world = 1;
+  float* count_host = nullptr;  // pinned: global count override
+  bool count_override = false;
+
+  // ------------------------------------------------------------------------------------
+  const void* W(int64_t off) const {
+    return act == DType::BF16 ? (const void*)(shadow + off) : (const void*)(params + off);
+  }
+  const float* P(int64_t off) const { return params + off; }
+  float* G(int64_t off) const { return grads + off; }
+  size_t es_() const { return dsize(act); }
+  void* at(void* base, int64_t elems) const { return (char*)base + elems * es_(); }
+
+  Drop mk_drop(float p, uint32_t site, bool on) const {
+    Drop d{};
+    if (!on || p <= 0.f) return d;
+    d.seed_ptr = seed;
+    d.site = site;
+    d.thresh = drop_threshold(p);
+    d.scale = 1.f / (1.f - p);
+    return d;
+  }
+  static uint32_t site(int dec, int layer, int kind) { return (uint32_t)((dec * 64 + layer) * 16 + kind); }
+
+  // C[M,N] = A[M,K] . W[N,K]^T  (nn.Linear)
+  void linear(const void* X, int64_t ldx, int64_t woff, int64_t ldw, void* C, int64_t ldc, DType tout, int M,
+              int N, int K, const float* bias, int relu, hipStream_t s) {
+    GemmArgs ga;
+    ga.M = M, ga.N = N, ga.K = K, ga.A = X, ga.lda = ldx, ga.B = W(woff), ga.ldb = ldw, ga.C = C, ga.ldc = ldc;
+    ga.bias = bias;
+    ga.relu = relu;
+    gemm(ga, act, tout, false, false, s);
+  }
+  // dX[M,K] (+)= alpha * dY[M,N] . W[N,K]
+  void linear_dx(const void* dY, int64_t ldy, int64_t woff, int64_t ldw, void* dX, int64_t ldx, int M, int N, int K,
+                 int beta, const void* relu_aux, const float* alpha_ptr, hipStream_t s) {
+    GemmArgs ga;
+    ga.M = M, ga.N = K, ga.K = N, ga.A = dY, ga.lda = ldy, ga.B = W(woff), ga.ldb = ldw, ga.C = dX, ga.ldc = ldx;
+    ga.beta = beta;
+    ga.aux = relu_aux;
+    ga.ldaux = ldx;
+    ga.alpha_ptr = alpha_ptr;
+    gemm(ga, act, act, false, true, s);
+  }
+  // dW[N,K] = alpha * dY[M,N]^T . X[M,K]   (f32, overwrites)
+  void linear_dw(const void* dY, int64_t ldy, const void* X, int64_t ldx, int64_t goff, int64_t ldg, int M, int N,
+                 int K, const float* alpha_ptr, hipStream_t s) {
+    GemmArgs ga;
+    ga.M = N, ga.N = K, ga.K = M, ga.A = dY, ga.lda = ldy, ga.B = X, ga.ldb = ldx, ga.C = G(goff), ga.ldc = ldg;
+    ga.alpha_ptr = alpha_ptr;
+    gemm(ga, act, DType::F32, true, true, s);
+  }
+
+  // ------------------------------------------------------------------------------------
+  void plan_acts(Planner& p, int B, int N, int T) {
+    const int64_t Me = (int64_t)B * N, L = T - 1, Md = (int64_t)B * L, d = L_().d, dd = L_().dd;
+    const int64_t Mx = std::max(Me, Md);
+    const size_t e = es_();
+    auto T_ = [&](void*& ptr, int64_t n) { ptr = p.raw(n * e); };
+    T_(a.Aenc, Me * L_().Kp);
+    p.take(a.valid, Me);
+    T_(a.ev0, Me * d);
+    p.take(a.em0, Me);
+    p.take(a.er0, Me);
+    a.X.resize(L_().Le + 1);
+    for (auto& x : a.X) T_(x, Me * d);
+    a.enc.resize(L_().Le);
+    for (auto& l : a.enc) {
+      T_(l.qkv, Me * 3 * d);
+      p.take(l.P, (size_t)B * L_().He * N * N);
+      T_(l.att, Me * d);
+      T_(l.v1, Me * d);
+      p.take(l.m1, Me);
+      p.take(l.r1, Me);
+      T_(l.Y, Me * d);
+      T_(l.H, Me * L_().fe);
+      T_(l.v2, Me * d);
+      p.take(l.m2, Me);
+      p.take(l.r2, Me);
+    }
+    T_(a.KV, Me * L_().Ld * 2 * dd);
+    p.take(a.ids, Md);
+    p.take(a.tgt, Md);
+    p.take(a.count, 4);
+    T_(a.E, Md * L_().dwe);
+    T_(a.dv0, Md * dd);
+    p.take(a.dm0, Md);
+    p.take(a.dr0, Md);
+    a.D.resize(L_().Ld + 1);
+    for (auto& x : a.D) T_(x, Md * dd);
+    a.dec.resize(L_().Ld);
+    for (auto& l : a.dec) {
+      T_(l.qkv, Md * 3 * dd);
+      p.take(l.Ps, (size_t)B * L_().Hd * L * L);
+      T_(l.atts, Md * dd);
+      T_(l.vs, Md * dd);
+      p.take(l.ms, Md);
+      p.take(l.rs, Md);
+      T_(l.D1, Md * dd);
+      T_(l.qc, Md * dd);
+      p.take(l.Pc, (size_t)B * L_().Hd * L * N);
+      T_(l.attc, Md * dd);
+      T_(l.vc, Md * dd);
+      p.take(l.mc, Md);
+      p.take(l.rc, Md);
+      T_(l.D2, Md * dd);
+      T_(l.H, Md * L_().fd);
+      T_(l.vf, Md * dd);
+      p.take(l.mf, Md);
+      p.take(l.rf, Md);
+    }
+    p.take(a.logits, Md * L_().V);
+    T_(a.dlogits, Md * L_().V);
+    p.take(a.loss_row, Md);
+    p.take(a.grad_scale, 4);
+    p.take(a.loss, 4);
+    const int64_t dmax = std::max<int64_t>(std::max(d, dd), L_().dwe);
+    T_(a.tmp, Mx * dmax);
+    T_(a.gOut, Mx * dmax);
+    T_(a.gRes, Mx * dmax);
+    T_(a.gA, Mx * dmax);
+    T_(a.gQKV, Mx * 3 * dmax);
+    T_(a.gATT, Mx * dmax);
+    T_(a.gH, Mx * std::max(L_().fe, L_().fd));
+    T_(a.gQc, Md * dd);
+    T_(a.gKV, Me * L_().Ld * 2 * dd);
+    T_(a.gE, Md * L_().dwe);
+  }
+  const Layout& L_() const { return L; }
+
+  void ensure_acts(int B, int N, int T) {
+    if (ws && B <= a.B && N <= a.N && T <= a.T) return;
+    int nB = std::max(B, a.B), nN = std::max(N, a.N), nT = std::max(T, a.T);
+    if (ws) {
+      CAPGEN_HIP(hipStreamSynchronize(es));
+      CAPGEN_HIP(hipFree(ws));
+      ws = nullptr;
+      drop_graph();
+    }
+    Planner p;
+    plan_acts(p, nB, nN, nT);
+    CAPGEN_HIP(hipMalloc(&ws, p.used));
+    Planner q;
+    q.base = (char*)ws;
+    plan_acts(q, nB, nN, nT);
+    a.B = nB, a.N = nN, a.T = nT;
+  }
+
+  void drop_graph() {
+    if (gexec) {
+      (void)hipGraphExecDestroy(gexec);
+      gexec = nullptr;
+    }
+  }
+
+  // ------------------------------------------------------------------------------------
+  // forward (model.py:79-98).  Always keeps the activations needed by backward.
+  void forward(const void* feats, DType ft, const float* pos, const int32_t* caps, int B, int N, int T,
+               float* loss_out, bool drop_on, hipStream_t s) {
+    require(B >= 1 && N >= 1 && T >= 2, "forward: need B>=1, N>=1, T>=2");
+    require(N <= 64 && T - 1 <= L.maxlen - 1, "forward: N must be <= 64 and T <= max_length");
+    const int Lq = T - 1, Me = B * N, Md = B * Lq, d = L.d, dd = L.dd;
+    const int He = L.He, Hd = L.Hd, dke = d / He, dkd = dd / Hd;
+    fB = B, fN = N, fT = T, fwd_drop = drop_on;
+    const float p = cfg.dropout, pa = cfg.attention_dropout;
+    if (drop_on) bump_seed(seed, s);
+
+    pack_encoder_input(feats, ft, pos, Me, L.F, L.P, L.Kp, a.Aenc, act, a.valid, s);
+    prepare_captions(caps, B, T, cfg.pad_idx, a.ids, a.tgt, a.count, s);
+    if (comm) {
+      if (count_override)
+        CAPGEN_HIP(hipMemcpyAsync(a.count, count_host, sizeof(float), hipMemcpyHostToDevice, s));
+      else
+        NCCL_CHECK(ncclAllReduce(a.count, a.count, 1, ncclFloat, ncclSum, comm, s));
+    }
+
+    // ---- encoder (model.py:294-332) ----
+    linear(a.Aenc, L.Kp, L.enc_emb_W, L.Kp, a.tmp, d, act, Me, d, L.Kp, nullptr, 0, s);
+    {
+      LnFwd ln;
+      ln.M = Me, ln.d = d, ln.a = a.tmp, ln.gamma = P(L.enc_lng), ln.beta = P(L.enc_lnb);
+      ln.y = a.X[0], ln.v_save = a.ev0, ln.mean = a.em0, ln.rstd = a.er0;
+      layernorm_fwd(ln, act, s);
+    }
+    RowMask emask{};
+    if (cfg.encode_mask) emask.valid = a.valid;
+    for (int l = 0; l < L.Le; ++l) {
+      const auto& w = L.enc[l];
+      auto& A = a.enc[l];
+      linear(a.X[l], d, w.Wqkv, d, A.qkv, 3 * d, act, Me, 3 * d, d, nullptr, 0, s);
+      AttnGeom g;
+      g.B = B, g.H = He, g.Lq = N, g.Lk = N, g.dk = dke;
+      g.q = A.qkv, g.q_ld = 3 * d, g.q_bs = (int64_t)N * 3 * d;
+      g.k = at(A.qkv, d), g.k_ld = 3 * d, g.k_bs = (int64_t)N * 3 * d;
+      g.v = at(A.qkv, 2 * d), g.v_ld = 3 * d, g.v_bs = (int64_t)N * 3 * d;
+      g.o_ld = d, g.o_bs = (int64_t)N * d;
+      if (cfg.encode_mask) {  // model.py:312-319: key-pad OR causal over regions
+        g.key_valid = a.valid, g.kv_bs = N, g.causal = 1;
+      }
+      g.temperature = std::sqrt((float)dke);
+      g.drop = mk_drop(pa, site(0, l, 0), drop_on);
+      attention_fwd(g, A.att, A.P, act, s);
+      linear(A.att, d, w.Wo, d, a.tmp, d, act, Me, d, d, nullptr, 0, s);
+      LnFwd l1;
+      l1.M = Me, l1.d = d, l1.a = a.tmp, l1.drop = mk_drop(p, site(0, l, 1), drop_on), l1.res = a.X[l];
+      l1.gamma = P(w.ln1g), l1.beta = P(w.ln1b), l1.y = A.Y, l1.v_save = A.v1, l1.mean = A.m1, l1.rstd = A.r1;
+      layernorm_fwd(l1, act, s);
+      linear(A.Y, d, w.W1, d, A.H, L.fe, act, Me, L.fe, d, P(w.b1), 1, s);
+      linear(A.H, L.fe, w.W2, L.fe, a.tmp, d, act, Me, d, L.fe, nullptr, 0, s);
+      LnFwd l2;
+      l2.M = Me, l2.d = d, l2.a = a.tmp, l2.a_bias = P(w.b2), l2.drop = mk_drop(p, site(0, l, 2), drop_on);
+      l2.res = A.Y, l2.gamma = P(w.ln2g), l2.beta = P(w.ln2b), l2.mask = emask;
+      l2.y = a.X[l + 1], l2.v_save = A.v2, l2.mean = A.m2, l2.rstd = A.r2;
+      layernorm_fwd(l2, act, s);
+    }
+    // cross-attention K/V of every decoder block in one GEMM over the encoder output
+    linear(a.X[L.Le], d, L.Wkv_all, d, a.KV, (int64_t)L.Ld * 2 * dd, act, Me, L.Ld * 2 * dd, d, nullptr, 0, s);
+
+    // ---- decoder (model.py:419-459) ----
+    embedding_gather(P(L.emb), a.ids, 1, Md, L.dwe, a.E, act, s);
+    linear(a.E, L.dwe, L.Wel, L.dwe, a.tmp, dd, act, Md, dd, L.dwe, nullptr, 0, s);
+    {
+      LnFwd ln;
+      ln.M = Md, ln.d = dd, ln.a = a.tmp, ln.pe = pe, ln.pe_L = Lq, ln.gamma = P(L.dec_lng), ln.beta = P(L.dec_lnb);
+      ln.y = a.D[0], ln.v_save = a.dv0, ln.mean = a.dm0, ln.rstd = a.dr0;
+      layernorm_fwd(ln, act, s);
+    }
+    RowMask dmask{};
+    dmask.ids = a.ids, dmask.pad_idx = cfg.pad_idx;
+    const int64_t kvld = (int64_t)L.Ld * 2 * dd;
+    for (int l = 0; l < L.Ld; ++l) {
+      const auto& w = L.dec[l];
+      auto& A = a.dec[l];
+      // self attention: key-pad(ids) OR causal (model.py:421-430)
+      linear(a.D[l], dd, w.Wqkv, dd, A.qkv, 3 * dd, act, Md, 3 * dd, dd, nullptr, 0, s);
+      AttnGeom g;
+      g.B = B, g.H = Hd, g.Lq = Lq, g.Lk = Lq, g.dk = dkd;
+      g.q = A.qkv, g.q_ld = 3 * dd, g.q_bs = (int64_t)Lq * 3 * dd;
+      g.k = at(A.qkv, dd), g.k_ld = 3 * dd, g.k_bs = (int64_t)Lq * 3 * dd;
+      g.v = at(A.qkv, 2 * dd), g.v_ld = 3 * dd, g.v_bs = (int64_t)Lq * 3 * dd;
+      g.o_ld = dd, g.o_bs = (int64_t)Lq * dd;
+      g.key_ids = a.ids, g.kid_bs = Lq, g.pad_idx = cfg.pad_idx, g.causal = 1;
+      g.temperature = std::sqrt((float)dkd);
+      g.drop = mk_drop(pa, site(1, l, 3), drop_on);
+      attention_fwd(g, A.atts, A.Ps, act, s);
+      linear(A.atts, dd, w.Wo_s, dd, a.tmp, dd, act, Md, dd, dd, nullptr, 0, s);
+      LnFwd l1;
+      l1.M = Md, l1.d = dd, l1.a = a.tmp, l1.drop = mk_drop(p, site(1, l, 4), drop_on), l1.res = a.D[l];
+      l1.gamma = P(w.lsg), l1.beta = P(w.lsb), l1.y = A.D1, l1.v_save = A.vs, l1.mean = A.ms, l1.rstd = A.rs;
+      layernorm_fwd(l1, act, s);
+      // cross attention over the encoder output, context mask = region key-pad (model.py:82)
+      linear(A.D1, dd, w.Wq_c, dd, A.qc, dd, act, Md, dd, dd, nullptr, 0, s);
+      AttnGeom c;
+      c.B = B, c.H = Hd, c.Lq = Lq, c.Lk = N, c.dk = dkd;
+      c.q = A.qc, c.q_ld = dd, c.q_bs = (int64_t)Lq * dd;
+      c.k = at(a.KV, (int64_t)l * 2 * dd), c.k_ld = kvld, c.k_bs = (int64_t)N * kvld;
+      c.v = at(a.KV, (int64_t)l * 2 * dd + dd), c.v_ld = kvld, c.v_bs = (int64_t)N * kvld;
+      c.o_ld = dd, c.o_bs = (int64_t)Lq * dd;
+      c.key_valid = a.valid, c.kv_bs = N;
+      c.temperature = std::sqrt((float)dkd);
+      c.drop = mk_drop(pa, site(1, l, 5), drop_on);
+      attention_fwd(c, A.attc, A.Pc, act, s);
+      linear(A.attc, dd, w.Wo_c, dd, a.tmp, dd, act, Md, dd, dd, nullptr, 0, s);
+      LnFwd l2;
+      l2.M = Md, l2.d = dd, l2.a = a.tmp, l2.drop = mk_drop(p, site(1, l, 6), drop_on), l2.res = A.D1;
+      l2.gamma = P(w.lcg), l2.beta = P(w.lcb), l2.y = A.D2, l2.v_save = A.vc, l2.mean = A.mc, l2.rstd = A.rc;
+      layernorm_fwd(l2, act, s);
+      // FFN, then x non_pad (modules.py:201-204)
+      linear(A.D2, dd, w.W1, dd, A.H, L.fd, act, Md, L.fd, dd, P(w.b1), 1, s);
+      linear(A.H, L.fd, w.W2, L.fd, a.tmp, dd, act, Md, dd, L.fd, nullptr, 0, s);
+      LnFwd l3;
+      l3.M = Md, l3.d = dd, l3.a = a.tmp, l3.a_bias = P(w.b2), l3.drop = mk_drop(p, site(1, l, 7), drop_on);
+      l3.res = A.D2, l3.gamma = P(w.lfg), l3.beta = P(w.lfb), l3.mask = dmask;
+      l3.y = a.D[l + 1], l3.v_save = A.vf, l3.mean = A.mf, l3.rstd = A.rf;
+      layernorm_fwd(l3, act, s);
+    }
+    // ---- classifier + CE (model.py:93-96) ----
+    linear(a.D[L.Ld], dd, L.Wc, dd, a.logits, L.V, DType::F32, Md, L.V, dd, P(L.bc), 0, s);
+    cross_entropy_rows(a.logits, a.tgt, Md, L.V, cfg.pad_idx, a.loss_row, a.dlogits, act, s);
+    loss_finalize(a.loss_row, Md, a.count, cfg.focal_loss, loss_out ? loss_out : a.loss, a.grad_scale, s);
+  }
+
+  // ------------------------------------------------------------------------------------
+  // one FFN + LayerNorm block backward; g_in = grad wrt block output, writes grad wrt the
+  // block input (residual) to r_out.  X = block input, H = hidden activations.
+  void ffn_bwd(int M, int d, int f, const void* g_in, const void* X, const void* H, const void* v, const float* mean,
+               const float* rstd, int64_t W1, int64_t b1, int64_t W2, int64_t b2, int64_t lng, int64_t lnb,
+               RowMask mask, Drop drop, void* r_out, hipStream_t s) {
+    LnBwd lb;
+    lb.M = M, lb.d = d, lb.dy = g_in, lb.v = v, lb.mean = mean, lb.rstd = rstd, lb.gamma = P(lng), lb.mask = mask;
+    lb.drop = drop, lb.d_res = r_out, lb.d_a = a.gA, lb.dgamma = G(lng), lb.dbeta = G(lnb);
+    layernorm_bwd(lb, act, s);
+    column_sum(a.gA, M, d, d, 1.f, nullptr, G(b2), act, s);
+    linear_dw(a.gA, d, H, f, W2, f, M, d, f, nullptr, s);
+    linear_dx(a.gA, d, W2, f, a.gH, f, M, d, f, 0, H, nullptr, s);  // x relu'(H)
+    column_sum(a.gH, M, f, f, 1.f, nullptr, G(b1), act, s);
+    linear_dw(a.gH, f, X, d, W1, d, M, f, d, nullptr, s);
+    linear_dx(a.gH, f, W1, d, r_out, d, M, f, d, 1, nullptr, nullptr, s);
+  }
+  // MHA output projection + LayerNorm backward: g_in = grad wrt LN output; writes grad wrt
+  // residual (query input) into r_out and grad wrt the attention output into a.gATT.
+  void mha_out_bwd(int M, int d, const void* g_in, const void* att, const void* v, const float* mean,
+                   const float* rstd, int64_t Wo, int64_t lng, int64_t lnb, Drop drop, void* r_out, hipStream_t s) {
+    LnBwd lb;
+    lb.M = M, lb.d = d, lb.dy = g_in, lb.v = v, lb.mean = mean, lb.rstd = rstd, lb.gamma = P(lng);
+    lb.drop = drop, lb.d_res = r_out, lb.d_a = a.gA, lb.dgamma = G(lng), lb.dbeta = G(lnb);
+    layernorm_bwd(lb, act, s);
+    linear_dw(a.gA, d, att, d, Wo, d, M, d, d, nullptr, s);
+    linear_dx(a.gA, d, Wo, d, a.gATT, d, M, d, d, 0, nullptr, nullptr, s);
+  }
+
+  void backward(hipStream_t s) {
+    require(fB > 0, "backward: call forward first");
+    const int B = fB, N = fN, Lq = fT - 1, Me = B * N, Md = B * Lq, d = L.d, dd = L.dd;
+    const int He = L.He, Hd = L.Hd, dke = d / He, dkd = dd / Hd;
+    const bool on = fwd_drop;
+    const float p = cfg.dropout, pa = cfg.attention_dropout;
+    // accumulated-gradient region (embedding table, LN params, biases) starts from zero
+    CAPGEN_HIP(hipMemsetAsync(grads + L.n_dense, 0, (L.total - L.n_dense) * sizeof(float), s));
+
+    // classifier: dlogits are unscaled (softmax - onehot); grad_scale folds 1/count (+focal)
+    column_sum(a.dlogits, Md, L.V, L.V, 1.f, a.grad_scale, G(L.bc), act, s);
+    linear_dw(a.dlogits, L.V, a.D[L.Ld], dd, L.Wc, dd, Md, L.V, dd, a.grad_scale, s);
+    linear_dx(a.dlogits, L.V, L.Wc, dd, a.gOut, dd, Md, L.V, dd, 0, nullptr, a.grad_scale, s);
+
+    RowMask dmask{};
+    dmask.ids = a.ids, dmask.pad_idx = cfg.pad_idx;
+    const int64_t kvld = (int64_t)L.Ld * 2 * dd;
+    void* gO = a.gOut;
+    void* gR = a.gRes;
+    for (int l = L.Ld - 1; l >= 0; --l) {
+      const auto& w = L.dec[l];
+      auto& A = a.dec[l];
+      ffn_bwd(Md, dd, L.fd, gO, A.D2, A.H, A.vf, A.mf, A.rf, w.W1, w.b1, w.W2, w.b2, w.lfg, w.lfb, dmask,
+              mk_drop(p, site(1, l, 7), on), gR, s);  // gR = grad wrt D2
+      mha_out_bwd(Md, dd, gR, A.attc, A.vc, A.mc, A.rc, w.Wo_c, w.lcg, w.lcb, mk_drop(p, site(1, l, 6), on), gO,
+                  s);  // gO = grad wrt D1 (residual part)
+      AttnGeom c;
+      c.B = B, c.H = Hd, c.Lq = Lq, c.Lk = N, c.dk = dkd;
+      c.q = A.qc, c.q_ld = dd, c.q_bs = (int64_t)Lq * dd;
+      c.k = at(a.KV, (int64_t)l * 2 * dd), c.k_ld = kvld, c.k_bs = (int64_t)N * kvld;
+      c.v = at(a.KV, (int64_t)l * 2 * dd + dd), c.v_ld = kvld, c.v_bs = (int64_t)N * kvld;
+      c.o_ld = dd, c.o_bs = (int64_t)Lq * dd;
+      c.temperature = std::sqrt((float)dkd);
+      c.drop = mk_drop(pa, site(1, l, 5), on);
+      attention_bwd(c, A.Pc, a.gATT, a.gQc, at(a.gKV, (int64_t)l * 2 * dd), at(a.gKV, (int64_t)l * 2 * dd + dd), act,
+                    s);
+      linear_dw(a.gQc, dd, A.D1, dd, w.Wq_c, dd, Md, dd, dd, nullptr, s);
+      linear_dx(a.gQc, dd, w.Wq_c, dd, gO, dd, Md, dd, dd, 1, nullptr, nullptr, s);  // gO = grad wrt D1
+      mha_out_bwd(Md, dd, gO, A.atts, A.vs, A.ms, A.rs, w.Wo_s, w.lsg, w.lsb, mk_drop(p, site(1, l, 4), on), gR,
+                  s);  // gR = grad wrt D_l (residual part)
+      AttnGeom g;
+      g.B = B, g.H = Hd, g.Lq = Lq, g.Lk = Lq, g.dk = dkd;
+      g.q = A.qkv, g.q_ld = 3 * dd, g.q_bs = (int64_t)Lq * 3 * dd;
+      g.k = at(A.qkv, dd), g.k_ld = 3 * dd, g.k_bs = (int64_t)Lq * 3 * dd;
+      g.v = at(A.qkv, 2 * dd), g.v_ld = 3 * dd, g.v_bs = (int64_t)Lq * 3 * dd;
+      g.o_ld = dd, g.o_bs = (int64_t)Lq * dd;
+      g.temperature = std::sqrt((float)dkd);
+      g.drop = mk_drop(pa, site(1, l, 3), on);
+      attention_bwd(g, A.Ps, a.gATT, a.gQKV, at(a.gQKV, dd), at(a.gQKV, 2 * dd), act, s);
+      linear_dw(a.gQKV, 3 * dd, a.D[l], dd, w.Wqkv, dd, Md, 3 * dd, dd, nullptr, s);
+      linear_dx(a.gQKV, 3 * dd, w.Wqkv, dd, gR, dd, Md, 3 * dd, dd, 1, nullptr, nullptr, s);
+      std::swap(gO, gR);  // gO = grad wrt D_l
+    }
+    // decoder embedding: LN(E.Wel^T + PE) (model.py:432-436)
+    {
+      LnBwd lb;
+      lb.M = Md, lb.d = dd, lb.dy = gO, lb.v = a.dv0, lb.mean = a.dm0, lb.rstd = a.dr0, lb.gamma = P(L.dec_lng);
+      lb.d_a = a.gA, lb.dgamma = G(L.dec_lng), lb.dbeta = G(L.dec_lnb);
+      layernorm_bwd(lb, act, s);
+      linear_dw(a.gA, dd, a.E, L.dwe, L.Wel, L.dwe, Md, dd, L.dwe, nullptr, s);
+      linear_dx(a.gA, dd, L.Wel, L.dwe, a.gE, L.dwe, Md, dd, L.dwe, 0, nullptr, nullptr, s);
+      embedding_scatter_add(a.gE, a.ids, Md, L.dwe, cfg.pad_idx, G(L.emb), act, s);
+    }
+    // cross K/V of all decoder blocks -> encoder output
+    linear_dw(a.gKV, kvld, a.X[L.Le], d, L.Wkv_all, d, Me, L.Ld * 2 * dd, d, nullptr, s);
+    gO = a.gOut;
+    gR = a.gRes;
+    linear_dx(a.gKV, kvld, L.Wkv_all, d, gO, d, Me, L.Ld * 2 * dd, d, 0, nullptr, nullptr, s);
+    RowMask emask{};
+    if (cfg.encode_mask) emask.valid = a.valid;
+    for (int l = L.Le - 1; l >= 0; --l) {
+      const auto& w = L.enc[l];
+      auto& A = a.enc[l];
+      ffn_bwd(Me, d, L.fe, gO, A.Y, A.H, A.v2, A.m2, A.r2, w.W1, w.b1, w.W2, w.b2, w.ln2g, w.ln2b, emask,
+              mk_drop(p, site(0, l, 2), on), gR, s);  // gR = grad wrt Y
+      mha_out_bwd(Me, d, gR, A.att, A.v1, A.m1, A.r1, w.Wo, w.ln1g, w.ln1b, mk_drop(p, site(0, l, 1), on), gO, s);
+      AttnGeom g;
+      g.B = B, g.H = He, g.Lq = N, g.Lk = N, g.dk = dke;
+      g.q = A.qkv, g.q_ld = 3 * d, g.q_bs = (int64_t)N * 3 * d;
+      g.k = at(A.qkv, d), g.k_ld = 3 * d, g.k_bs = (int64_t)N * 3 * d;
+      g.v = at(A.qkv, 2 * d), g.v_ld = 3 * d, g.v_bs = (int64_t)N * 3 * d;
+      g.o_ld = d, g.o_bs = (int64_t)N * d;
+      if (cfg.encode_mask) g.key_valid = a.valid, g.kv_bs = N, g.causal = 1;
+      g.temperature = std::sqrt((float)dke);
+      g.drop = mk_drop(pa, site(0, l, 0), on);
+      attention_bwd(g, A.P, a.gATT, a.gQKV, at(a.gQKV, d), at(a.gQKV, 2 * d), act, s);
+      linear_dw(a.gQKV, 3 * d, a.X[l], d, w.Wqkv, d, Me, 3 * d, d, nullptr, s);
+      linear_dx(a.gQKV, 3 * d, w.Wqkv, d, gO, d, Me, 3 * d, d, 1, nullptr, nullptr, s);  // gO = grad wrt X_l
+    }
+    {
+      LnBwd lb;
+      lb.M = Me, lb.d = d, lb.dy = gO, lb.v = a.ev0, lb.mean = a.em0, lb.rstd = a.er0, lb.gamma = P(L.enc_lng);
+      lb.d_a = a.gA, lb.dgamma = G(L.enc_lng), lb.dbeta = G(L.enc_lnb);
+      layernorm_bwd(lb, act, s);
+      linear_dw(a.gA, d, a.Aenc, L.Kp, L.enc_emb_W, L.Kp, Me, d, L.Kp, nullptr, s);
+    }
+  }
+
+  void allreduce_grads(hipStream_t s) {
+    if (!comm) return;
+    NCCL_CHECK(ncclAllReduce(grads, grads, (size_t)L.total, ncclFloat, ncclSum, comm, s));
+  }
+
+  void adam(hipStream_t s) {
+    adam_prepare(step, cfg.lr, cfg.beta1, cfg.beta2, adam_scal, s);
+    adam_update(params, grads, am, av, (size_t)L.total, cfg.beta1, cfg.beta2, cfg.eps, adam_scal, shadow,
+                shadow ? (size_t)L.n_dense : 0, s);
+  }
+
+  void refresh_shadow(hipStream_t s) {
+    if (shadow) to_bf16(params, shadow, (size_t)L.n_dense, s);
+  }
+
+  // ------------------------------------------------------------------------------------
+  // stream hand-off: caller stream -> engine stream -> caller stream
+  void enter(hipStream_t cs) {
+    CAPGEN_HIP(hipEventRecord(ev_in, cs));
+    CAPGEN_HIP(hipStreamWaitEvent(es, ev_in, 0));
+  }
+  void leave(hipStream_t cs) {
+    CAPGEN_HIP(hipEventRecord(ev_out, es));
+    CAPGEN_HIP(hipStreamWaitEvent(cs, ev_out, 0));
+  }
+
+  void train_step(const void* f, DType ft, const float* pos, const int32_t* caps, int B, int N, int T, float* loss,
+                  hipStream_t cs) {
+    ensure_acts(B, N, T);
+    enter(cs);
+    Key k{f, pos, caps, loss, (int)ft, B, N, T, training};
+    auto body = [&]() {
+      forward(f, ft, pos, caps, B, N, T, loss, training, es);
+      backward(es);
+      allreduce_grads(es);
+      adam(es);
+    };
+    if (!graph_on) {
+      body();
+    } else {
+      if (!(gexec && gkey == k)) {
+        drop_graph();
+        hipGraph_t graph = nullptr;
+        CAPGEN_HIP(hipStreamBeginCapture(es, hipStreamCaptureModeThreadLocal));
+        try {
+          body();
+        } catch (...) {
+          (void)hipStreamEndCapture(es, &graph);
+          if (graph) (void)hipGraphDestroy(graph);
+          throw;
+        }
+        CAPGEN_HIP(hipStreamEndCapture(es, &graph));
+        CAPGEN_HIP(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
+        CAPGEN_HIP(hipGraphDestroy(graph));
+        gkey = k;
+      }
+      CAPGEN_HIP(hipGraphLaunch(gexec, es));
+    }
+    leave(cs);
+  }
+
+  // ------------------------------------------------------------------------------------
+  // decoding (model.py:101-200), KV-cached.  Bit-identical to recomputing the prefix: row
+  // results of every kernel are independent of how many rows/positions are in the launch.
+  void encode_only(const void* feats, DType ft, const float* pos, int B, int N, hipStream_t s) {
+    const int Me = B * N, d = L.d, He = L.He, dke = d / He;
+    ensure_acts(B, N, 2);
+    pack_encoder_input(feats, ft, pos, Me, L.F, L.P, L.Kp, a.Aenc, act, a.valid, s);
+    linear(a.Aenc, L.Kp, L.enc_emb_W, L.Kp, a.tmp, d, act, Me, d, L.Kp, nullptr, 0, s);
+    LnFwd ln;
+    ln.M = Me, ln.d = d, ln.a = a.tmp, ln.gamma = P(L.enc_lng), ln.beta = P(L.enc_lnb), ln.y = a.X[0];
+    layernorm_fwd(ln, act, s);
+    RowMask emask{};
+    if (cfg.encode_mask) emask.valid = a.valid;
+    for (int l = 0; l < L.Le; ++l) {
+      const auto& w = L.enc[l];
+      auto& A = a.enc[l];
+      linear(a.X[l], d, w.Wqkv, d, A.qkv, 3 * d, act, Me, 3 * d, d, nullptr, 0, s);
+      AttnGeom g;
+      g.B = B, g.H = He, g.Lq = N, g.Lk = N, g.dk = dke;
+      g.q = A.qkv, g.q_ld = 3 * d, g.q_bs = (int64_t)N * 3 * d;
+      g.k = at(A.qkv, d), g.k_ld = 3 * d, g.k_bs = (int64_t)N * 3 * d;
+      g.v = at(A.qkv, 2 * d), g.v_ld = 3 * d, g.v_bs = (int64_t)N * 3 * d;
+      g.o_ld = d, g.o_bs = (int64_t)N * d;
+      if (cfg.encode_mask) g.key_valid = a.valid, g.kv_bs = N, g.causal = 1;
+      g.temperature = std::sqrt((float)dke);
+      attention_fwd(g, A.att, nullptr, act, s);
+      linear(A.att, d, w.Wo, d, a.tmp, d, act, Me, d, d, nullptr, 0, s);
+      LnFwd l1;
+      l1.M = Me, l1.d = d, l1.a = a.tmp, l1.res = a.X[l], l1.gamma = P(w.ln1g), l1.beta = P(w.ln1b), l1.y = A.Y;
+      layernorm_fwd(l1, act, s);
+      linear(A.Y, d, w.W1, d, A.H, L.fe, act, Me, L.fe, d, P(w.b1), 1, s);
+      linear(A.H, L.fe, w.W2, L.fe, a.tmp, d, act, Me, d, L.fe, nullptr, 0, s);
+      LnFwd l2;
+      l2.M = Me, l2.d = d, l2.a = a.tmp, l2.a_bias = P(w.b2), l2.res = A.Y, l2.gamma = P(w.ln2g);
+      l2.beta = P(w.ln2b), l2.mask = emask, l2.y = a.X[l + 1];
+      layernorm_fwd(l2, act, s);
+    }
+    linear(a.X[L.Le], d, L.Wkv_all, d, a.KV, (int64_t)L.Ld * 2 * L.dd, act, Me, L.Ld * 2 * L.dd, d, nullptr, 0, s);
+  }
+
+  void plan_gen(Planner& p, int R, int N) {
+    const int64_t dd = L.dd, Tc = L.maxlen, e = es_();
+    auto T_ = [&](void*& ptr, int64_t n) { ptr = p.raw(n * e); };
+    T_(g.x, R * dd);
+    T_(g.x1, R * dd);
+    T_(g.x2, R * dd);
+    T_(g.q, R * dd);
+    T_(g.att, R * dd);
+    T_(g.tmp, R * std::max<int64_t>(dd, L.dwe));
+    T_(g.h, (int64_t)R * L.fd);
+    T_(g.E, (int64_t)R * L.dwe);
+    p.take(g.mean, R);
+    p.take(g.rstd, R);
+    p.take(g.Pc, (size_t)R * L.Hd * N);
+    p.take(g.logits, (size_t)R * L.V);
+    p.take(g.probs, (size_t)R * L.V);
+    T_(g.cache, (int64_t)L.Ld * R * Tc * 2 * dd);
+    T_(g.cache2, (int64_t)L.Ld * R * Tc * 2 * dd);
+    p.take(g.ids, (size_t)R * Tc);
+    p.take(g.ids2, (size_t)R * Tc);
+    p.take(g.seq, (size_t)R * Tc);
+    p.take(g.seq2, (size_t)R * Tc);
+    p.take(g.bprob, R);
+    p.take(g.bprob2, R);
+    p.take(g.bsrc, R);
+    p.take(g.btok, R);
+  }
+  void ensure_gen(int R, int N) {
+    if (gws && R <= g.R && N <= g.N) return;
+    int nR = std::max(R, g.R), nN = std::max(N, g.N);
+    if (gws) {
+      CAPGEN_HIP(hipStreamSynchronize(es));
+      CAPGEN_HIP(hipFree(gws));
+      gws = nullptr;
+    }
+    Planner p;
+    plan_gen(p, nR, nN);
+    CAPGEN_HIP(hipMalloc(&gws, p.used));
+    Planner q;
+    q.base = (char*)gws;
+    plan_gen(q, nR, nN);
+    g.R = nR, g.N = nN;
+  }
+
+  // decoder for position t of R rows (rows r -> image r % Bimg); tokens = ids[:, t].
+  // Leaves logits [R, V] in g.logits; cross-attn probs of the last block in g.Pc if want_attn.
+  void dec_step(int R, int Bimg, int N, int t, void* cache, const int32_t* ids, bool want_attn, hipStream_t s) {
+    const int dd = L.dd, Hd = L.Hd, dkd = dd / Hd, Tc = L.maxlen;
+    embedding_gather(P(L.emb), ids + t, Tc, R, L.dwe, g.E, act, s);
+    linear(g.E, L.dwe, L.Wel, L.dwe, g.tmp, dd, act, R, dd, L.dwe, nullptr, 0, s);
+    LnFwd ln;
+    ln.M = R, ln.d = dd, ln.a = g.tmp, ln.pe = pe + (int64_t)t * dd, ln.pe_L = 1, ln.gamma = P(L.dec_lng);
+    ln.beta = P(L.dec_lnb), ln.y = g.x;
+    layernorm_fwd(ln, act, s);
+    RowMask rm{};
+    rm.ids = ids + t, rm.ids_ld = Tc, rm.pad_idx = cfg.pad_idx;
+    const int64_t kvld = (int64_t)L.Ld * 2 * dd, cld = (int64_t)Tc * 2 * dd;
+    for (int l = 0; l < L.Ld; ++l) {
+      const auto& w = L.dec[l];
+      void* cl = at(cache, (int64_t)l * R * cld);
+      linear(g.x, dd, w.Wqkv, dd, g.q, dd, act, R, dd, dd, nullptr, 0, s);
+      linear(g.x, dd, w.Wqkv + (int64_t)dd * dd, dd, at(cl, (int64_t)t * 2 * dd), cld, act, R, 2 * dd, dd, nullptr, 0,
+             s);
+      AttnGeom sg;
+      sg.B = R, sg.H = Hd, sg.Lq = 1, sg.Lk = t + 1, sg.dk = dkd;
+      sg.q = g.q, sg.q_ld = dd, sg.q_bs = dd;
+      sg.k = cl, sg.k_ld = 2 * dd, sg.k_bs = cld;
+      sg.v = at(cl, dd), sg.v_ld = 2 * dd, sg.v_bs = cld;
+      sg.o_ld = dd, sg.o_bs = dd;
+      sg.key_ids = ids, sg.kid_bs = Tc, sg.pad_idx = cfg.pad_idx, sg.causal = 1, sg.q_pos0 = t;
+      sg.temperature = std::sqrt((float)dkd);
+      attention_fwd(sg, g.att, nullptr, act, s);
+      linear(g.att, dd, w.Wo_s, dd, g.tmp, dd, act, R, dd, dd, nullptr, 0, s);
+      LnFwd l1;
+      l1.M = R, l1.d = dd, l1.a = g.tmp, l1.res = g.x, l1.gamma = P(w.lsg), l1.beta = P(w.lsb), l1.y = g.x1;
+      layernorm_fwd(l1, act, s);
+      linear(g.x1, dd, w.Wq_c, dd, g.q, dd, act, R, dd, dd, nullptr, 0, s);
+      AttnGeom c;
+      c.B = R, c.H = Hd, c.Lq = 1, c.Lk = N, c.dk = dkd;
+      c.q = g.q, c.q_ld = dd, c.q_bs = dd;
+      c.k = at(a.KV, (int64_t)l * 2 * dd), c.k_ld = kvld, c.k_bs = (int64_t)N * kvld;
+      c.v = at(a.KV, (int64_t)l * 2 * dd + dd), c.v_ld = kvld, c.v_bs = (int64_t)N * kvld;
+      c.kv_bmod = Bimg;
+      c.o_ld = dd, c.o_bs = dd;
+      c.key_valid = a.valid, c.kv_bs = N;
+      c.temperature = std::sqrt((float)dkd);
+      attention_fwd(c, g.att, (want_attn && l == L.Ld - 1) ? g.Pc : nullptr, act, s);
+      linear(g.att, dd, w.Wo_c, dd, g.tmp, dd, act, R, dd, dd, nullptr, 0, s);
+      LnFwd l2;
+      l2.M = R, l2.d = dd, l2.a = g.tmp, l2.res = g.x1, l2.gamma = P(w.lcg), l2.beta = P(w.lcb), l2.y = g.x2;
+      layernorm_fwd(l2, act, s);
+      linear(g.x2, dd, w.W1, dd, g.h, L.fd, act, R, L.fd, dd, P(w.b1), 1, s);
+      linear(g.h, L.fd, w.W2, L.fd, g.tmp, dd, act, R, dd, L.fd, nullptr, 0, s);
+      LnFwd l3;
+      l3.M = R, l3.d = dd, l3.a = g.tmp, l3.a_bias = P(w.b2), l3.res = g.x2, l3.gamma = P(w.lfg), l3.beta = P(w.lfb);
+      l3.mask = rm, l3.y = g.x;
+      layernorm_fwd(l3, act, s);
+    }
+    linear(g.x, dd, L.Wc, dd, g.logits, L.V, DType::F32, R, L.V, dd, P(L.bc), 0, s);
+  }
+
+  void greedy(const void* feats, DType ft, const float* pos, int B, int N, int64_t* ids_out, float* attn_out,
+              hipStream_t s) {
+    require(N >= 1 && N <= 64, "greedy: N must be in [1, 64]");
+    encode_only(feats, ft, pos, B, N, s);
+    ensure_gen(B, N);
+    const int Tc = L.maxlen, W = L.maxlen + 1;
+    init_gen_ids_kernel<<<(B * std::max(W, Tc) + 255) / 256, 256, 0, s>>>(ids_out, B, W, g.ids, Tc);
+    CAPGEN_HIP(hipGetLastError());
+    for (int t = 0; t < L.maxlen - 1; ++t) {
+      dec_step(B, B, N, t, g.cache, g.ids, attn_out != nullptr, s);
+      if (attn_out) attention_head_mean(g.Pc, B, L.Hd, 1, N, 0, attn_out + (int64_t)t * B * N, s);
+      argmax_softmax(g.logits, B, L.V, ids_out, W, t + 1, g.ids + t + 1, Tc, s);
+    }
+  }
+
+  void beam(const void* feats, DType ft, const float* pos, int B, int N, int k, int64_t* ids_out, hipStream_t s) {
+    require(k >= 1 && k <= 16, "beam_search: beam_size must be in [1, 16]");
+    require(k <= L.V, "beam_search: beam_size must be <= num_vocab");
+    const int R = k * B, Tc = L.maxlen, Tw = L.maxlen, dd = L.dd;
+    encode_only(feats, ft, pos, B, N, s);
+    ensure_gen(R, N);
+    init_gen_ids_kernel<<<(R * Tc + 255) / 256, 256, 0, s>>>(g.seq, R, Tw, g.ids, Tc);
+    CAPGEN_HIP(hipGetLastError());
+    // position 0: every beam holds <START>; top-k of beam 0's distribution (model.py:148-166)
+    dec_step(R, B, N, 0, g.cache, g.ids, false, s);
+    softmax_rows(g.logits, R, L.V, g.probs, s);
+    beam_topk_kernel<<<B, 256, 0, s>>>(g.probs, nullptr, 1, B, L.V, k, g.bprob, g.bsrc, g.btok);
+    CAPGEN_HIP(hipGetLastError());
+    CAPGEN_HIP(hipMemsetAsync(g.bsrc, 0, sizeof(int32_t) * R, s));  // all beams descend from beam 0 at t = 0
+    auto reorder = [&](int t) {
+      // seq/ids rows follow their source beam, then column t+1 = chosen token
+      dim3 gs(1, R);
+      beam_gather_kernel<int64_t><<<gs, 64, 0, s>>>(g.seq, g.seq2, Tw, Tw, g.bsrc, B, R, g.btok, t + 1);
+      beam_gather_kernel<int32_t><<<gs, 64, 0, s>>>(g.ids, g.ids2, Tc, Tc, g.bsrc, B, R, g.btok, t + 1);
+      const int64_t cld = (int64_t)Tc * 2 * dd;
+      for (int l = 0; l < L.Ld; ++l) {
+        dim3 gc(std::min<int64_t>(((int64_t)(t + 1) * 2 * dd + 255) / 256, 64), R);
+        if (act == DType::F32)
+          beam_gather_kernel<float><<<gc, 256, 0, s>>>((const float*)at(g.cache, l * R * cld),
+                                                       (float*)at(g.cache2, l * R * cld), cld, (int64_t)(t + 1) * 2 * dd,
+                                                       g.bsrc, B, R, nullptr, 0);
+        else
+          beam_gather_kernel<bf16><<<gc, 256, 0, s>>>((const bf16*)at(g.cache, l * R * cld),
+                                                      (bf16*)at(g.cache2, l * R * cld), cld, (int64_t)(t + 1) * 2 * dd,
+                                                      g.bsrc, B, R, nullptr, 0);
+      }
+      CAPGEN_HIP(hipGetLastError());
+      std::swap(g.seq, g.seq2);
+      std::swap(g.ids, g.ids2);
+      std::swap(g.cache, g.cache2);
+    };
+    reorder(0);
+    for (int t = 1; t < Tw - 1; ++t) {
+      dec_step(R, B, N, t, g.cache, g.ids, false, s);
+      softmax_rows(g.logits, R, L.V, g.probs, s);
+      beam_topk_kernel<<<B, 256, 0, s>>>(g.probs, g.bprob, k, B, L.V, k, g.bprob2, g.bsrc, g.btok);
+      CAPGEN_HIP(hipGetLastError());
+      std::swap(g.bprob, g.bprob2);
+      reorder(t);
+    }
+    CAPGEN_HIP(hipMemcpyAsync(ids_out, g.seq, sizeof(int64_t) * B * Tw, hipMemcpyDeviceToDevice, s));
+  }
+
+  ~capgen_engine() {
+    if (es) (void)hipStreamSynchronize(es);
+    drop_graph();
+    if (comm) ncclCommDestroy(comm);
+    for (void* p : {(void*)params, (void*)grads, (void*)am, (void*)av, (void*)shadow, (void*)pe, (void*)step,
+                    (void*)adam_scal, (void*)seed, (void*)scalars, ws, gws})
+      if (p) (void)hipFree(p);
+    if (count_host) (void)hipHostFree(count_host);
+    if (ev_in) (void)hipEventDestroy(ev_in);
+    if (ev_out) (void)hipEventDestroy(ev_out);
+    if (es) (void)hipStreamDestroy(es);
+  }
+};
+
+// =========================================================================================
+// C ABI
+// =========================================================================================
+namespace {
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    f();
+    return 0;
+  } catch (const Error& e) {
+    g_last_error = e.msg;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+  } catch (...) {
+    g_last_error = "unknown error";
+  }
+  return 1;
+}
+
+DType dt(int x) {
+  require(x == CAPGEN_F32 || x == CAPGEN_BF16, "dtype must be CAPGEN_F32 or CAPGEN_BF16");
+  return x == CAPGEN_F32 ? DType::F32 : DType::BF16;
+}
+
+void set_device(capgen_t* h) {
+  require(h != nullptr, "null engine handle");
+  CAPGEN_HIP(hipSetDevice(h->device));
+}
+
+void pe_table(const Layout& L, std::vector<float>& out) {
+  // model.py:502-514: float64 angles, sin on even columns, cos on odd, cast to f32
+  const int n = L.maxlen - 1, d = L.dd;
+  out.resize((size_t)n * d);
+  for (int p = 0; p < n; ++p)
+    for (int j = 0; j < d; ++j) {
+      double ang = (double)p / std::pow(10000.0, 2.0 * (j / 2) / (double)d);
+      out[(size_t)p * d + j] = (float)((j % 2 == 0) ? std::sin(ang) : std::cos(ang));
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* capgen_last_error(void) { return g_last_error.c_str(); }
+int capgen_abi_version(void) { return CAPGEN_ABI_VERSION; }
+
+int capgen_param_table(const capgen_config* cfg, capgen_param_info* out, int cap, int* count, int64_t* arena_elems) {
+  return guarded([&] {
+    require(cfg != nullptr, "null config");
+    Layout L = make_layout(*cfg);
+    if (count) *count = (int)L.table.size();
+    if (arena_elems) *arena_elems = L.total;
+    for (int i = 0; i < (int)L.table.size() && i < cap && out; ++i) out[i] = L.table[i];
+  });
+}
+
+int capgen_create(const capgen_config* cfg, int device, capgen_t** out) {
+  return guarded([&] {
+    require(cfg && out, "null argument");
+    *out = nullptr;
+    int ndev = 0;
+    CAPGEN_HIP(hipGetDeviceCount(&ndev));
+    require(device >= 0 && device < ndev, "capgen_create: invalid device index");
+    CAPGEN_HIP(hipSetDevice(device));
+    auto h = std::make_unique<capgen_engine>();
+    h->cfg = *cfg;
+    h->L = make_layout(*cfg);
+    h->device = device;
+    h->act = dt(cfg->dtype);
+    const size_t n = (size_t)h->L.total;
+    CAPGEN_HIP(hipStreamCreateWithFlags(&h->es, hipStreamNonBlocking));
+    CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
+    CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming));
+    CAPGEN_HIP(hipMalloc(&h->params, n * 4));
+    CAPGEN_HIP(hipMalloc(&h->grads, n * 4));
+    CAPGEN_HIP(hipMalloc(&h->am, n * 4));
+    CAPGEN_HIP(hipMalloc(&h->av, n * 4));
+    CAPGEN_HIP(hipMemset(h->params, 0, n * 4));
+    CAPGEN_HIP(hipMemset(h->grads, 0, n * 4));
+    CAPGEN_HIP(hipMemset(h->am, 0, n * 4));
+    CAPGEN_HIP(hipMemset(h->av, 0, n * 4));
+    if (h->act == DType::BF16) {
+      CAPGEN_HIP(hipMalloc(&h->shadow, (size_t)h->L.n_dense * 2));
+      CAPGEN_HIP(hipMemset(h->shadow, 0, (size_t)h->L.n_dense * 2));
+    }
+    std::vector<float> pe;
+    pe_table(h->L, pe);
+    CAPGEN_HIP(hipMalloc(&h->pe, pe.size() * 4));
+    CAPGEN_HIP(hipMemcpy(h->pe, pe.data(), pe.size() * 4, hipMemcpyHostToDevice));
+    CAPGEN_HIP(hipMalloc(&h->step, 64));
+    CAPGEN_HIP(hipMemset(h->step, 0, 64));
+    CAPGEN_HIP(hipMalloc(&h->adam_scal, 64));
+    CAPGEN_HIP(hipMalloc(&h->seed, 64));
+    uint64_t sd = cfg->seed;
+    CAPGEN_HIP(hipMemcpy(h->seed, &sd, 8, hipMemcpyHostToDevice));
+    CAPGEN_HIP(hipMalloc(&h->scalars, 256));
+    CAPGEN_HIP(hipHostMalloc(&h->count_host, 64, hipHostMallocDefault));
+    *out = h.release();
+  });
+}
+
+int capgen_destroy(capgen_t* h) {
+  return guarded([&] {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    delete h;
+  });
+}
+
+int capgen_get_params(capgen_t* h, float* dst, int64_t n) {
+  return guarded([&] {
+    set_device(h);
+    require(n == h->L.total, "get_params: size mismatch");
+    CAPGEN_HIP(hipStreamSynchronize(h->es));
+    CAPGEN_HIP(hipMemcpy(dst, h->params, n * 4, hipMemcpyDeviceToHost));
+  });
+}
+
+int capgen_set_params(capgen_t* h, const float* src, int64_t n) {
+  return guarded([&] {
+    set_device(h);
+    require(n == h->L.total, "set_params: size mismatch");
+    CAPGEN_HIP(hipStreamSynchronize(h->es));
+    CAPGEN_HIP(hipMemcpy(h->params, src, n * 4, hipMemcpyHostToDevice));
+    h->refresh_shadow(h->es);
+    CAPGEN_HIP(hipStreamSynchronize(h->es));
+  });
+}
+
+int capgen_get_grads(capgen_t* h, float* dst, int64_t n) {
+  return guarded([&] {
+    set_device(h);
+    require(n == h->L.total, "get_grads: size mismatch");
+    CAPGEN_HIP(hipStreamSynchronize(h->es));
+    CAPGEN_HIP(hipMemcpy(dst, h->grads, n * 4, hipMemcpyDeviceToHost));
+  });
+}
+
+int capgen_get_adam_state(capgen_t* h, int64_t* step, float* m, float* v, int64_t n) {
+  return guarded([&] {
+    set_device(h);
+    require(n == h->L.total, "get_adam_state: size mismatch");
+    CAPGEN_HIP(hipStreamSynchronize(h->es));
+    if (step) CAPGEN_HIP(hipMemcpy(step, h->step, 8, hipMemcpyDeviceToHost));
+    if (m) CAPGEN_HIP(hipMemcpy(m, h->am, n * 4, hipMemcpyDeviceToHost));
+    if (v) CAPGEN_HIP(hipMemcpy(v, h->av, n * 4, hipMemcpyDeviceToHost));
+  });
+}
+
+int capgen_set_adam_state(capgen_t* h, int64_t step, const float* m, const float* v, int64_t n) {
+  return guarded([&] {
+    set_device(h);
+    require(n == h->L.total, "set_adam_state: size mismatch");
+    CAPGEN_HIP(hipStreamSynchronize(h->es));
+    CAPGEN_HIP(hipMemcpy(h->step, &step, 8, hipMemcpyHostToDevice));
+    if (m) CAPGEN_HIP(hipMemcpy(h->am, m, n * 4, hipMemcpyHostToDevice));
+    else CAPGEN_HIP(hipMemset(h->am, 0, n * 4));
+    if (v) CAPGEN_HIP(hipMemcpy(h->av, v, n * 4, hipMemcpyHostToDevice));
+    else CAPGEN_HIP(hipMemset(h->av, 0, n * 4));
+  });
+}
+
+int capgen_arenas(capgen_t* h, float** params, float** grads, int64_t* n) {
+  return guarded([&] {
+    require(h != nullptr, "null engine handle");
+    if (params) *params = h->params;
+    if (grads) *grads = h->grads;
+    if (n) *n = h->L.total;
+  });
+}
+
+int capgen_set_training(capgen_t* h, int training) {
+  return guarded([&] {
+    require(h != nullptr, "null engine handle");
+    h->training = training != 0;
+  });
+}
+
+int capgen_set_graph(capgen_t* h, int enable) {
+  return guarded([&] {
+    require(h != nullptr, "null engine handle");
+    h->graph_on = enable != 0;
+    if (!h->graph_on) h->drop_graph();
+  });
+}
+
+int capgen_forward(capgen_t* h, const void* feats, int ft, const float* pos, const int32_t* caps, int B, int N, int T,
+                   float* loss_out, void* stream) {
+  return guarded([&] {
+    set_device(h);
+    hipStream_t cs = (hipStream_t)stream;
+    h->ensure_acts(B, N, T);
+    h->enter(cs);
+    h->forward(feats, dt(ft), pos, caps, B, N, T, loss_out, h->training, h->es);
+    h->leave(cs);
+  });
+}
+
+int capgen_backward(capgen_t* h, void* stream) {
+  return guarded([&] {
+    set_device(h);
+    hipStream_t cs = (hipStream_t)stream;
+    h->enter(cs);
+    h->backward(h->es);
+    h->allreduce_grads(h->es);
+    h->leave(cs);
+  });
+}
+
+int capgen_adam_step(capgen_t* h, void* stream) {
+  return guarded([&] {
+    set_device(h);
+    hipStream_t cs = (hipStream_t)stream;
+    h->enter(cs);
+    h->adam(h->es);
+    h->leave(cs);
+  });
+}
+
+int capgen_train_step(capgen_t* h, const void* feats, int ft, const float* pos, const int32_t* caps, int B, int N,
+                      int T, float* loss_out, void* stream) {
+  return guarded([&] {
+    set_device(h);
+    h->train_step(feats, dt(ft), pos, caps, B, N, T, loss_out, (hipStream_t)stream);
+  });
+}
+
+int capgen_compute_loss(capgen_t* h, const void* feats, int ft, const float* pos, const int32_t* caps, int B, int N,
+                        int T, float* loss_out, void* stream) {
+  // torch.no_grad() only: dropout follows the module's train/eval state (models.py:131-135)
+  return capgen_forward(h, feats, ft, pos, caps, B, N, T, loss_out, stream);
+}
+
+int capgen_copy_logits(capgen_t* h, float* dst, int64_t n, void* stream) {
+  return guarded([&] {
+    set_device(h);
+    require(h->fB > 0, "copy_logits: no forward yet");
+    const int64_t want = (int64_t)h->fB * (h->fT - 1) * h->L.V;
+    require(n == want, "copy_logits: size mismatch");
+    hipStream_t cs = (hipStream_t)stream;
+    h->enter(cs);
+    CAPGEN_HIP(hipMemcpyAsync(dst, h->a.logits, n * 4, hipMemcpyDeviceToDevice, h->es));
+    h->leave(cs);
+  });
+}
+
+int capgen_greedy(capgen_t* h, const void* feats, int ft, const float* pos, int B, int N, int64_t* ids_out,
+                  float* attn_out, void* stream) {
+  return guarded([&] {
+    set_device(h);
+    hipStream_t cs = (hipStream_t)stream;
+    h->enter(cs);
+    h->greedy(feats, dt(ft), pos, B, N, ids_out, attn_out, h->es);
+    h->leave(cs);
+  });
+}
+
+int capgen_beam(capgen_t* h, const void* feats, int ft, const float* pos, int B, int N, int k, int64_t* ids_out,
+                void* stream) {
+  return guarded([&] {
+    set_device(h);
+    hipStream_t cs = (hipStream_t)stream;
+    h->enter(cs);
+    h->beam(feats, dt(ft), pos, B, N, k, ids_out, h->es);
+    h->leave(cs);
+  });
+}
+
+int capgen_set_rng_seed(capgen_t* h, uint64_t sd) {
+  return guarded([&] {
+    set_device(h);
+    CAPGEN_HIP(hipStreamSynchronize(h->es));
+    CAPGEN_HIP(hipMemcpy(h->seed, &sd, 8, hipMemcpyHostToDevice));
+  });
+}
+
+int capgen_debug_gemm(int M, int N, int K, const void* A, int64_t lda, int ta, const void* B, int64_t ldb, int tb,
+                      void* Cp, int64_t ldc, int in_dtype, int out_dtype, const float* bias, float alpha, int beta,
+                      int relu, void* stream) {
+  return guarded([&] {
+    GemmArgs ga;
+    ga.M = M, ga.N = N, ga.K = K, ga.A = A, ga.lda = lda, ga.B = B, ga.ldb = ldb, ga.C = Cp, ga.ldc = ldc;
+    ga.bias = bias, ga.alpha = alpha, ga.beta = beta, ga.relu = relu;
+    gemm(ga, dt(in_dtype), dt(out_dtype), ta != 0, tb != 0, (hipStream_t)stream);
+  });
+}
+
+int capgen_dp_unique_id(char out[128]) {
+  return guarded([&] {
+    ncclUniqueId id;
+    NCCL_CHECK(ncclGetUniqueId(&id));
+    std::memcpy(out, id.internal, 128);
+  });
+}
+
+int capgen_dp_init(capgen_t* h, const char id[128], int rank, int world) {
+  return guarded([&] {
+    set_device(h);
+    require(world >= 1 && rank >= 0 && rank < world, "dp_init: bad rank/world");
+    require(!h->cfg.focal_loss || world == 1, "dp_init: FocalLoss needs the global mean CE; not supported with DP");
+    ncclUniqueId uid;
+    std::memcpy(uid.internal, id, 128);
+    if (h->comm) ncclCommDestroy(h->comm);
+    NCCL_CHECK(ncclCommInitRank(&h->comm, world, uid, rank));
+    h->rank = rank, h->world = world;
+    h->drop_graph();
+    // replicate rank 0's parameters
+    NCCL_CHECK(ncclBroadcast(h->params, h->params, (size_t)h->L.total, ncclFloat, 0, h->comm, h->es));
+    h->refresh_shadow(h->es);
+    CAPGEN_HIP(hipStreamSynchronize(h->es));
+  });
+}
+
+int capgen_dp_set_global_count(capgen_t* h, float count) {
+  return guarded([&] {
+    require(h != nullptr, "null engine handle");
+    h->count_override = count > 0.f;
+    *h->count_host = count;
+  });
+}
+
+}  // extern "C"

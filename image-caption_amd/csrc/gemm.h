@@ -1,0 +1,31 @@
+// capgen — GEMM launcher interface (see gemm.hip for the kernel).
+#pragma once
+#include "capgen_common.h"
+
+namespace capgen {
+
+enum class DType : int { F32 = 0, BF16 = 1 };
+
+inline size_t dsize(DType t) { return t == DType::F32 ? 4 : 2; }
+
+struct GemmArgs {
+  int M = 0, N = 0, K = 0;
+  const void* A = nullptr;
+  int64_t lda = 0;
+  const void* B = nullptr;
+  int64_t ldb = 0;
+  void* C = nullptr;
+  int64_t ldc = 0;
+  const float* bias = nullptr;      // [N] f32, added before relu
+  const void* aux = nullptr;        // same dtype as A/B: zero the output where aux[m][n] <= 0
+  int64_t ldaux = 0;
+  float alpha = 1.f;
+  const float* alpha_ptr = nullptr;  // device scalar multiplied into alpha (e.g. 1/count)
+  int beta = 0;                      // 1: accumulate into C
+  int relu = 0;
+};
+
+// ta: A stored [K][M] (else [M][K]); tb: B stored [K][N] (else [N][K]).
+void gemm(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t s);
+
+}  // namespace capgen

@@ -1,0 +1,230 @@
+// capgen — MFMA GEMM for gfx950 with fused epilogues.
+//
+//   C[m][n] = epi( alpha * sum_k opA(m,k) * opB(k,n) )
+//   opA(m,k) = TA ? A[k*lda + m] : A[m*lda + k]
+//   opB(k,n) = TB ? B[k*ldb + n] : B[n*ldb + k]        (TB=0 is nn.Linear's W[N][K])
+//   epi: (+ bias[n]) -> (* (aux[m][n] > 0)) -> relu -> (+ C_old if beta)
+//
+// Forward projections are NT (X . W^T), input gradients NN (dY . W), weight gradients
+// TN (dY^T . X).  bf16 operands use v_mfma_f32_16x16x32_bf16; the fp32 parity mode
+// uses v_mfma_f32_16x16x4_f32 (an exact f32 fma chain).  Accumulation is always f32.
+//
+// Tiling: 256 threads = 4 wave64s in a 2x2 grid over a BMxBN tile, BK = 32, two LDS
+// buffers with register-staged global loads (issue next tile's loads before the MFMAs of
+// the current tile, write them to the other LDS buffer after).  Transposed operands are
+// transposed on the LDS write so every MFMA fragment is one 16-B ds_read (bf16).
+#include "gemm.h"
+
+namespace capgen {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+template <typename T> struct GemmTraits;
+template <> struct GemmTraits<float> {
+  static constexpr int VEC = 4;  // elements per 16-B global load
+  static constexpr int PAD = 4;
+};
+template <> struct GemmTraits<bf16> {
+  static constexpr int VEC = 8;
+  static constexpr int PAD = 8;
+};
+
+constexpr int BK = 32;
+constexpr int NTHREADS = 256;
+
+template <typename T, bool TRANS, int ROWS>
+struct TileLoader {
+  // Stage a ROWS x BK tile (rows = M or N index, cols = k) into registers, then LDS [ROWS][LDK].
+  static constexpr int VEC = GemmTraits<T>::VEC;
+  static constexpr int LDK = BK + GemmTraits<T>::PAD;
+  static constexpr int NV = ROWS * BK / VEC / NTHREADS;  // vectors per thread
+  static_assert(NV >= 1, "tile too small");
+  typedef typename Vec16<T>::type V;
+  V reg[NV];
+
+  __device__ __forceinline__ void load(const T* __restrict__ src, int64_t ld, int r0, int R, int k0,
+                                       int K, int tid) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      int v = tid + i * NTHREADS;
+      int r, k;
+      bool ok;
+      const T* p;
+      if constexpr (!TRANS) {
+        r = v / (BK / VEC);
+        k = (v % (BK / VEC)) * VEC;
+        ok = (r0 + r < R) && (k0 + k < K);
+        p = src + (int64_t)(r0 + r) * ld + (k0 + k);
+      } else {
+        k = v / (ROWS / VEC);
+        r = (v % (ROWS / VEC)) * VEC;
+        ok = (k0 + k < K) && (r0 + r < R);
+        p = src + (int64_t)(k0 + k) * ld + (r0 + r);
+      }
+      if (ok) {
+        reg[i] = *reinterpret_cast<const V*>(p);
+      } else {
+        reg[i] = V{};
+      }
+    }
+  }
+  __device__ __forceinline__ void store(T* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      int v = tid + i * NTHREADS;
+      if constexpr (!TRANS) {
+        int r = v / (BK / VEC);
+        int k = (v % (BK / VEC)) * VEC;
+        *reinterpret_cast<V*>(lds + r * LDK + k) = reg[i];
+      } else {
+        int k = v / (ROWS / VEC);
+        int r = (v % (ROWS / VEC)) * VEC;
+        const T* e = reinterpret_cast<const T*>(&reg[i]);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) lds[(r + j) * LDK + k] = e[j];
+      }
+    }
+  }
+};
+
+template <typename T, typename TO, bool TA, bool TB, int BM, int BN>
+__global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs g) {
+  constexpr int LDK = BK + GemmTraits<T>::PAD;
+  constexpr int FM = BM / 32, FN = BN / 32;  // 16x16 fragments per wave
+  __shared__ __attribute__((aligned(16))) T As[2][BM * LDK];
+  __shared__ __attribute__((aligned(16))) T Bs[2][BN * LDK];
+
+  const T* __restrict__ A = reinterpret_cast<const T*>(g.A);
+  const T* __restrict__ B = reinterpret_cast<const T*>(g.B);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+
+  TileLoader<T, TA, BM> la;
+  TileLoader<T, TB, BN> lb;
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (g.K + BK - 1) / BK;
+  la.load(A, g.lda, m0, g.M, 0, g.K, tid);
+  lb.load(B, g.ldb, n0, g.N, 0, g.K, tid);
+  la.store(As[0], tid);
+  lb.store(Bs[0], tid);
+  __syncthreads();
+
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      la.load(A, g.lda, m0, g.M, (kt + 1) * BK, g.K, tid);
+      lb.load(B, g.ldb, n0, g.N, (kt + 1) * BK, g.K, tid);
+    }
+    const T* as = As[cur] + (wm * (BM / 2) + fr) * LDK;
+    const T* bs = Bs[cur] + (wn * (BN / 2) + fr) * LDK;
+    if constexpr (sizeof(T) == 2) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(as + i * 16 * LDK + fq * 8);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(bs + j * 16 * LDK + fq * 8);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < BK / 4; ++ks) {
+        float af[FM], bfr[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[i] = to_f(as[i * 16 * LDK + ks * 4 + fq]);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bfr[j] = to_f(bs[j * 16 * LDK + ks * 4 + fq]);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (kt + 1 < nk) {
+      la.store(As[cur ^ 1], tid);
+      lb.store(Bs[cur ^ 1], tid);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue ----
+  const float alpha = g.alpha_ptr ? g.alpha * *g.alpha_ptr : g.alpha;
+  TO* __restrict__ C = reinterpret_cast<TO*>(g.C);
+  const T* __restrict__ aux = reinterpret_cast<const T*>(g.aux);
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wn * (BN / 2) + j * 16 + fr;
+      if (n >= g.N) continue;
+      const float bn = g.bias ? g.bias[n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * (BM / 2) + i * 16 + fq * 4 + r;
+        if (m >= g.M) continue;
+        float v = alpha * acc[i][j][r] + bn;
+        if (aux && !(to_f(aux[(int64_t)m * g.ldaux + n]) > 0.f)) v = 0.f;
+        if (g.relu) v = fmaxf(v, 0.f);
+        TO* cp = C + (int64_t)m * g.ldc + n;
+        if (g.beta) v += to_f(*cp);
+        *cp = from_f<TO>(v);
+      }
+    }
+  }
+}
+
+template <typename T, typename TO, bool TA, bool TB>
+static void launch_tiles(const GemmArgs& g, hipStream_t s) {
+  // Pick the largest tile that still gives >= ~1 block per CU (256 CUs).
+  auto blocks = [&](int bm, int bn) { return (long)((g.M + bm - 1) / bm) * ((g.N + bn - 1) / bn); };
+  if (blocks(128, 128) >= 240) {
+    dim3 grid((g.N + 127) / 128, (g.M + 127) / 128);
+    gemm_kernel<T, TO, TA, TB, 128, 128><<<grid, NTHREADS, 0, s>>>(g);
+  } else if (blocks(128, 64) >= 240) {
+    dim3 grid((g.N + 63) / 64, (g.M + 127) / 128);
+    gemm_kernel<T, TO, TA, TB, 128, 64><<<grid, NTHREADS, 0, s>>>(g);
+  } else {
+    dim3 grid((g.N + 63) / 64, (g.M + 63) / 64);
+    gemm_kernel<T, TO, TA, TB, 64, 64><<<grid, NTHREADS, 0, s>>>(g);
+  }
+}
+
+template <typename T, typename TO>
+static void launch_layout(const GemmArgs& g, bool ta, bool tb, hipStream_t s) {
+  if (!ta && !tb) launch_tiles<T, TO, false, false>(g, s);
+  else if (!ta && tb) launch_tiles<T, TO, false, true>(g, s);
+  else if (ta && !tb) launch_tiles<T, TO, true, false>(g, s);
+  else launch_tiles<T, TO, true, true>(g, s);
+}
+
+void gemm(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t s) {
+  if (g.M <= 0 || g.N <= 0) return;
+  const int vec = in == DType::F32 ? 4 : 8;
+  // the contiguous dimension of each operand is read in 16-B vectors
+  require((ta ? g.M : g.K) % vec == 0 && g.lda % vec == 0, "gemm: A contiguous dim/ld not a multiple of 16 B");
+  require((tb ? g.N : g.K) % vec == 0 && g.ldb % vec == 0, "gemm: B contiguous dim/ld not a multiple of 16 B");
+  require(((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0, "gemm: operands must be 16-B aligned");
+  require(g.K > 0, "gemm: K must be positive");
+  if (in == DType::F32) {
+    if (out == DType::F32) launch_layout<float, float>(g, ta, tb, s);
+    else launch_layout<float, bf16>(g, ta, tb, s);
+  } else {
+    if (out == DType::F32) launch_layout<bf16, float>(g, ta, tb, s);
+    else launch_layout<bf16, bf16>(g, ta, tb, s);
+  }
+  CAPGEN_HIP(hipGetLastError());
+}
+
+}  // namespace capgen

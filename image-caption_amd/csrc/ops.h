@@ -1,0 +1,86 @@
+// capgen — row-wise / elementwise / optimizer kernels (launcher interface).
+#pragma once
+#include "capgen_common.h"
+#include "gemm.h"
+
+namespace capgen {
+
+// Row mask applied to a LayerNorm output / its gradient: row m is zeroed when
+// ids[m] == pad (decoder non_pad_mask, model.py:483-486) or valid[m] == 0 (encoder
+// non_pad_mask with encode_mask, model.py:356-359).
+struct RowMask {
+  const int32_t* ids = nullptr;
+  int64_t ids_ld = 1;  // ids of row m at ids[m * ids_ld]
+  int pad_idx = 0;
+  const uint8_t* valid = nullptr;
+};
+
+// y = LN(drop(a + a_bias) + res + pe[m % pe_L]) * rowmask          (modules.py:86-90, 114-120)
+struct LnFwd {
+  int M = 0, d = 0;
+  const void* a = nullptr;
+  const float* a_bias = nullptr;
+  Drop drop{};
+  const void* res = nullptr;
+  const float* pe = nullptr;
+  int pe_L = 1;
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+  RowMask mask{};
+  void* y = nullptr;
+  void* v_save = nullptr;  // LN input (post residual add), saved for backward
+  float* mean = nullptr;
+  float* rstd = nullptr;
+};
+void layernorm_fwd(const LnFwd& a, DType t, hipStream_t s);
+
+struct LnBwd {
+  int M = 0, d = 0;
+  const void* dy = nullptr;
+  const void* v = nullptr;
+  const float* mean = nullptr;
+  const float* rstd = nullptr;
+  const float* gamma = nullptr;
+  RowMask mask{};
+  Drop drop{};             // the dropout applied to `a` in the forward
+  void* d_res = nullptr;   // grad wrt residual input (= grad wrt LN input), or null
+  void* d_a = nullptr;     // grad wrt a (dropout mask applied), or null
+  float* dgamma = nullptr;  // accumulated
+  float* dbeta = nullptr;   // accumulated
+};
+void layernorm_bwd(const LnBwd& a, DType t, hipStream_t s);
+
+// out[m] = [feats[m] | pos[m] | 0] (width Kp), valid[m] = any(pos[m] != 0)  (model.py:202-209)
+void pack_encoder_input(const void* feats, DType feats_t, const float* pos, int M, int F, int P, int Kp,
+                        void* out, DType out_t, uint8_t* valid, hipStream_t s);
+// caps [B][T] -> ids_in [B][T-1], tgt [B][T-1]; count = #(tgt != pad) as f32   (model.py:88-89)
+void prepare_captions(const int32_t* caps, int B, int T, int pad, int32_t* ids_in, int32_t* tgt,
+                      float* count, hipStream_t s);
+// out[m] = table[ids[m]] (f32 table -> T)                                      (model.py:432)
+void embedding_gather(const float* table, const int32_t* ids, int64_t ids_ld, int M, int d, void* out, DType t,
+                      hipStream_t s);
+// grad[ids[m]] += dE[m] for ids[m] != pad  (nn.Embedding padding_idx)
+void embedding_scatter_add(const void* dE, const int32_t* ids, int M, int d, int pad, float* grad, DType t,
+                           hipStream_t s);
+// db[n] += alpha (* *alpha_ptr) * sum_m X[m][n]
+void column_sum(const void* X, int M, int N, int64_t ldx, float alpha, const float* alpha_ptr, float* db,
+                DType t, hipStream_t s);
+// per-row cross entropy: loss_row[m] = lse - logit[tgt], dlogits = softmax - onehot (unscaled, 0 for pad)
+void cross_entropy_rows(const float* logits, const int32_t* tgt, int M, int V, int pad, float* loss_row,
+                        void* dlogits, DType t, hipStream_t s);
+// loss = sum(loss_row)/count (or FocalLoss of it); grad_scale = dloss/d(logit sums)
+void loss_finalize(const float* loss_row, int M, const float* count, int focal, float* loss_out,
+                   float* grad_scale, hipStream_t s);
+// Adam (torch.optim.Adam semantics).  step_buf: int64 step counter (incremented here).
+void adam_prepare(int64_t* step, float lr, float b1, float b2, float* scal, hipStream_t s);
+void adam_update(float* p, const float* g, float* m, float* v, size_t n, float b1, float b2, float eps,
+                 const float* scal, bf16* shadow, size_t n_shadow, hipStream_t s);
+void to_bf16(const float* src, bf16* dst, size_t n, hipStream_t s);
+// greedy: out token = argmax(softmax(logits[b])) (first index on ties)   (model.py:126-128)
+void argmax_softmax(const float* logits, int B, int V, int64_t* ids_out, int64_t ids_ld, int col,
+                    int32_t* next_ids, int64_t next_ld, hipStream_t s);
+// softmax probabilities [B][V] (for beam search)
+void softmax_rows(const float* logits, int B, int V, float* probs, hipStream_t s);
+void bump_seed(uint64_t* seed, hipStream_t s);
+
+}  // namespace capgen

@@ -1,0 +1,523 @@
+// capgen — row-wise / elementwise / optimizer kernels for gfx950.
+//
+// LayerNorm: one wave64 per row (d/64 contiguous elements per lane, 16-B loads), the
+// mean/var reductions are cross-lane shuffles; dropout/bias/residual/positional-encoding
+// adds and the non-pad row mask are fused in.  Backward accumulates dgamma/dbeta per
+// workgroup and issues one f32 atomic per column per workgroup.
+// CE: one workgroup per row (V=10000 f32 logits stay in L2 for the 3 passes).
+// Adam: 16-B vectorised streaming over the flat parameter arena (HBM bound).
+#include "ops.h"
+
+namespace capgen {
+
+constexpr int LN_THREADS = 256;  // 4 rows per workgroup
+constexpr float LN_EPS = 1e-6f;  // modules.py:57,105
+
+__device__ __forceinline__ bool row_kept(const RowMask& rm, int m) {
+  if (rm.ids && rm.ids[(int64_t)m * rm.ids_ld] == rm.pad_idx) return false;
+  if (rm.valid && !rm.valid[m]) return false;
+  return true;
+}
+
+template <typename T, int DPL>
+__global__ void __launch_bounds__(LN_THREADS) ln_fwd_kernel(LnFwd a) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * (LN_THREADS / 64) + (threadIdx.x >> 6);
+  if (m >= a.M) return;
+  const int d = a.d, c0 = lane * DPL;
+  const int64_t base = (int64_t)m * d + c0;
+  float x[DPL];
+  load_f<T, DPL>(reinterpret_cast<const T*>(a.a) + base, x);
+  if (a.a_bias) {
+#pragma unroll
+    for (int e = 0; e < DPL; ++e) x[e] += a.a_bias[c0 + e];
+  }
+  if (a.drop.seed_ptr) {
+    const uint64_t seed = *a.drop.seed_ptr;
+#pragma unroll
+    for (int e = 0; e < DPL; ++e)
+      x[e] = drop_keep(seed, a.drop.site, (uint32_t)(base + e), a.drop.thresh) ? x[e] * a.drop.scale : 0.f;
+  }
+  if (a.res) {
+    float r[DPL];
+    load_f<T, DPL>(reinterpret_cast<const T*>(a.res) + base, r);
+#pragma unroll
+    for (int e = 0; e < DPL; ++e) x[e] += r[e];
+  }
+  if (a.pe) {
+    const float* pe = a.pe + (int64_t)(m % a.pe_L) * d + c0;
+#pragma unroll
+    for (int e = 0; e < DPL; ++e) x[e] += pe[e];
+  }
+  if (a.v_save) store_f<T, DPL>(reinterpret_cast<T*>(a.v_save) + base, x);
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < DPL; ++e) s += x[e];
+  const float mean = wave_sum(s) / (float)d;
+  float q = 0.f;
+#pragma unroll
+  for (int e = 0; e < DPL; ++e) {
+    float t = x[e] - mean;
+    q = fmaf(t, t, q);
+  }
+  const float var = wave_sum(q) / (float)d;
+  const float rstd = 1.0f / sqrtf(var + LN_EPS);
+  const float keep = row_kept(a.mask, m) ? 1.f : 0.f;
+  float y[DPL];
+#pragma unroll
+  for (int e = 0; e < DPL; ++e) y[e] = ((x[e] - mean) * rstd * a.gamma[c0 + e] + a.beta[c0 + e]) * keep;
+  store_f<T, DPL>(reinterpret_cast<T*>(a.y) + base, y);
+  if (lane == 0) {
+    if (a.mean) a.mean[m] = mean;
+    if (a.rstd) a.rstd[m] = rstd;
+  }
+}
+
+template <typename T, int DPL>
+__global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(LnBwd a) {
+  __shared__ float red[2][LN_THREADS / 64][64 * DPL];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int d = a.d, c0 = lane * DPL;
+  float dg[DPL], db[DPL];
+#pragma unroll
+  for (int e = 0; e < DPL; ++e) dg[e] = db[e] = 0.f;
+  const uint64_t seed = a.drop.seed_ptr ? *a.drop.seed_ptr : 0;
+  for (int m = blockIdx.x * (LN_THREADS / 64) + wave; m < a.M; m += gridDim.x * (LN_THREADS / 64)) {
+    const int64_t base = (int64_t)m * d + c0;
+    float dy[DPL], v[DPL];
+    load_f<T, DPL>(reinterpret_cast<const T*>(a.dy) + base, dy);
+    load_f<T, DPL>(reinterpret_cast<const T*>(a.v) + base, v);
+    const float mean = a.mean[m], rstd = a.rstd[m];
+    const float keep = row_kept(a.mask, m) ? 1.f : 0.f;
+    float g[DPL], xh[DPL], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < DPL; ++e) {
+      dy[e] *= keep;
+      xh[e] = (v[e] - mean) * rstd;
+      g[e] = dy[e] * a.gamma[c0 + e];
+      s1 += g[e];
+      s2 = fmaf(g[e], xh[e], s2);
+      dg[e] = fmaf(dy[e], xh[e], dg[e]);
+      db[e] += dy[e];
+    }
+    const float mg = wave_sum(s1) / (float)d, mgx = wave_sum(s2) / (float)d;
+    float dv[DPL];
+#pragma unroll
+    for (int e = 0; e < DPL; ++e) dv[e] = rstd * (g[e] - mg - xh[e] * mgx);
+    if (a.d_res) store_f<T, DPL>(reinterpret_cast<T*>(a.d_res) + base, dv);
+    if (a.d_a) {
+      if (a.drop.seed_ptr) {
+#pragma unroll
+        for (int e = 0; e < DPL; ++e)
+          dv[e] = drop_keep(seed, a.drop.site, (uint32_t)(base + e), a.drop.thresh) ? dv[e] * a.drop.scale : 0.f;
+      }
+      store_f<T, DPL>(reinterpret_cast<T*>(a.d_a) + base, dv);
+    }
+  }
+  if (!a.dgamma) return;
+#pragma unroll
+  for (int e = 0; e < DPL; ++e) {
+    red[0][wave][c0 + e] = dg[e];
+    red[1][wave][c0 + e] = db[e];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < d; c += LN_THREADS) {
+    float sg = 0.f, sb = 0.f;
+#pragma unroll
+    for (int w = 0; w < LN_THREADS / 64; ++w) {
+      sg += red[0][w][c];
+      sb += red[1][w][c];
+    }
+    atomicAdd(a.dgamma + c, sg);
+    atomicAdd(a.dbeta + c, sb);
+  }
+}
+
+template <typename T>
+static void ln_fwd_dispatch(const LnFwd& a, hipStream_t s) {
+  dim3 grid((a.M + 3) / 4);
+  switch (a.d / 64) {
+    case 1: ln_fwd_kernel<T, 1><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 2: ln_fwd_kernel<T, 2><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 4: ln_fwd_kernel<T, 4><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 8: ln_fwd_kernel<T, 8><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 16: ln_fwd_kernel<T, 16><<<grid, LN_THREADS, 0, s>>>(a); break;
+    default: throw Error("layernorm: width must be 64 * {1,2,4,8,16}");
+  }
+}
+void layernorm_fwd(const LnFwd& a, DType t, hipStream_t s) {
+  if (a.M <= 0) return;
+  if (t == DType::F32) ln_fwd_dispatch<float>(a, s);
+  else ln_fwd_dispatch<bf16>(a, s);
+  CAPGEN_HIP(hipGetLastError());
+}
+
+template <typename T>
+static void ln_bwd_dispatch(const LnBwd& a, hipStream_t s) {
+  const int rows_per_block = 32;  // 8 rows per wave -> fewer dgamma atomics
+  dim3 grid((a.M + rows_per_block - 1) / rows_per_block);
+  switch (a.d / 64) {
+    case 1: ln_bwd_kernel<T, 1><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 2: ln_bwd_kernel<T, 2><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 4: ln_bwd_kernel<T, 4><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 8: ln_bwd_kernel<T, 8><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 16: ln_bwd_kernel<T, 16><<<grid, LN_THREADS, 0, s>>>(a); break;
+    default: throw Error("layernorm: width must be 64 * {1,2,4,8,16}");
+  }
+}
+void layernorm_bwd(const LnBwd& a, DType t, hipStream_t s) {
+  if (a.M <= 0) return;
+  if (t == DType::F32) ln_bwd_dispatch<float>(a, s);
+  else ln_bwd_dispatch<bf16>(a, s);
+  CAPGEN_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------------------
+template <typename TI, typename TO>
+__global__ void pack_kernel(const TI* __restrict__ feats, const float* __restrict__ pos, int F, int P, int Kp,
+                            TO* __restrict__ out, uint8_t* __restrict__ valid) {
+  __shared__ int nz;
+  const int m = blockIdx.x;
+  if (threadIdx.x == 0) nz = 0;
+  __syncthreads();
+  const TI* f = feats + (int64_t)m * F;
+  const float* p = pos + (int64_t)m * P;
+  TO* o = out + (int64_t)m * Kp;
+  for (int c = threadIdx.x; c < Kp; c += blockDim.x) {
+    float x;
+    if (c < F) x = to_f(f[c]);
+    else if (c < F + P) {
+      x = p[c - F];
+      if (x != 0.f) atomicOr(&nz, 1);
+    } else x = 0.f;
+    o[c] = from_f<TO>(x);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) valid[m] = nz ? 1 : 0;
+}
+
+void pack_encoder_input(const void* feats, DType ft, const float* pos, int M, int F, int P, int Kp, void* out,
+                        DType ot, uint8_t* valid, hipStream_t s) {
+  if (M <= 0) return;
+  dim3 grid(M);
+  if (ft == DType::F32 && ot == DType::F32)
+    pack_kernel<float, float><<<grid, 256, 0, s>>>((const float*)feats, pos, F, P, Kp, (float*)out, valid);
+  else if (ft == DType::F32 && ot == DType::BF16)
+    pack_kernel<float, bf16><<<grid, 256, 0, s>>>((const float*)feats, pos, F, P, Kp, (bf16*)out, valid);
+  else if (ft == DType::BF16 && ot == DType::BF16)
+    pack_kernel<bf16, bf16><<<grid, 256, 0, s>>>((const bf16*)feats, pos, F, P, Kp, (bf16*)out, valid);
+  else
+    pack_kernel<bf16, float><<<grid, 256, 0, s>>>((const bf16*)feats, pos, F, P, Kp, (float*)out, valid);
+  CAPGEN_HIP(hipGetLastError());
+}
+
+__global__ void prep_caps_kernel(const int32_t* __restrict__ caps, int B, int T, int pad, int32_t* ids_in,
+                                 int32_t* tgt, float* count) {
+  __shared__ int cnt;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  const int L = T - 1;
+  int local = 0;
+  for (int c = threadIdx.x; c < B * L; c += blockDim.x) {
+    int b = c / L, t = c % L;
+    ids_in[c] = caps[b * T + t];
+    int y = caps[b * T + t + 1];
+    tgt[c] = y;
+    local += (y != pad);
+  }
+  atomicAdd(&cnt, local);
+  __syncthreads();
+  if (threadIdx.x == 0) *count = (float)cnt;
+}
+
+void prepare_captions(const int32_t* caps, int B, int T, int pad, int32_t* ids_in, int32_t* tgt, float* count,
+                      hipStream_t s) {
+  prep_caps_kernel<<<1, 1024, 0, s>>>(caps, B, T, pad, ids_in, tgt, count);
+  CAPGEN_HIP(hipGetLastError());
+}
+
+template <typename T>
+__global__ void gather_kernel(const float* __restrict__ table, const int32_t* __restrict__ ids, int64_t ids_ld,
+                              int M, int d, T* __restrict__ out) {
+  int64_t n = (int64_t)M * d;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x) {
+    int64_t m = c / d;
+    int col = c % d;
+    out[c] = from_f<T>(table[(int64_t)ids[m * ids_ld] * d + col]);
+  }
+}
+void embedding_gather(const float* table, const int32_t* ids, int64_t ids_ld, int M, int d, void* out, DType t,
+                      hipStream_t s) {
+  if (M <= 0) return;
+  int64_t n = (int64_t)M * d;
+  int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  if (t == DType::F32) gather_kernel<float><<<grid, 256, 0, s>>>(table, ids, ids_ld, M, d, (float*)out);
+  else gather_kernel<bf16><<<grid, 256, 0, s>>>(table, ids, ids_ld, M, d, (bf16*)out);
+  CAPGEN_HIP(hipGetLastError());
+}
+
+template <typename T>
+__global__ void scatter_kernel(const T* __restrict__ dE, const int32_t* __restrict__ ids, int M, int d, int pad,
+                               float* __restrict__ grad) {
+  int64_t n = (int64_t)M * d;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x) {
+    int64_t m = c / d;
+    int id = ids[m];
+    if (id == pad) continue;
+    atomicAdd(grad + (int64_t)id * d + (c % d), to_f(dE[c]));
+  }
+}
+void embedding_scatter_add(const void* dE, const int32_t* ids, int M, int d, int pad, float* grad, DType t,
+                           hipStream_t s) {
+  if (M <= 0) return;
+  int64_t n = (int64_t)M * d;
+  int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  if (t == DType::F32) scatter_kernel<float><<<grid, 256, 0, s>>>((const float*)dE, ids, M, d, pad, grad);
+  else scatter_kernel<bf16><<<grid, 256, 0, s>>>((const bf16*)dE, ids, M, d, pad, grad);
+  CAPGEN_HIP(hipGetLastError());
+}
+
+template <typename T>
+__global__ void colsum_kernel(const T* __restrict__ X, int M, int N, int64_t ldx, float alpha,
+                              const float* alpha_ptr, float* __restrict__ db) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float acc = 0.f;
+  for (int m = blockIdx.y; m < M; m += gridDim.y) acc += to_f(X[(int64_t)m * ldx + n]);
+  const float a = alpha_ptr ? alpha * *alpha_ptr : alpha;
+  atomicAdd(db + n, a * acc);
+}
+void column_sum(const void* X, int M, int N, int64_t ldx, float alpha, const float* alpha_ptr, float* db, DType t,
+                hipStream_t s) {
+  if (M <= 0 || N <= 0) return;
+  dim3 grid((N + 255) / 256, std::min(32, (M + 31) / 32));
+  if (t == DType::F32) colsum_kernel<float><<<grid, 256, 0, s>>>((const float*)X, M, N, ldx, alpha, alpha_ptr, db);
+  else colsum_kernel<bf16><<<grid, 256, 0, s>>>((const bf16*)X, M, N, ldx, alpha, alpha_ptr, db);
+  CAPGEN_HIP(hipGetLastError());
+}
+
+// ---- block reductions (256 threads = 4 waves) ----
+__device__ __forceinline__ float block_max(float v, float* sh) {
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float r = fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
+  __syncthreads();
+  return r;
+}
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float r = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+  __syncthreads();
+  return r;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) ce_kernel(const float* __restrict__ logits, const int32_t* __restrict__ tgt,
+                                                 int V, int pad, float* __restrict__ loss_row, T* __restrict__ dl) {
+  __shared__ float sh[4];
+  const int m = blockIdx.x;
+  const float* x = logits + (int64_t)m * V;
+  T* g = dl + (int64_t)m * V;
+  const int y = tgt[m];
+  if (y == pad) {
+    for (int c = threadIdx.x; c < V; c += 256) g[c] = from_f<T>(0.f);
+    if (threadIdx.x == 0) loss_row[m] = 0.f;
+    return;
+  }
+  float mx = -INFINITY;
+  for (int c = threadIdx.x; c < V; c += 256) mx = fmaxf(mx, x[c]);
+  mx = block_max(mx, sh);
+  float se = 0.f;
+  for (int c = threadIdx.x; c < V; c += 256) se += expf(x[c] - mx);
+  se = block_sum(se, sh);
+  const float inv = 1.f / se;
+  for (int c = threadIdx.x; c < V; c += 256) {
+    float p = expf(x[c] - mx) * inv;
+    g[c] = from_f<T>(p - (c == y ? 1.f : 0.f));
+  }
+  if (threadIdx.x == 0) loss_row[m] = (logf(se) + mx) - x[y];
+}
+void cross_entropy_rows(const float* logits, const int32_t* tgt, int M, int V, int pad, float* loss_row, void* dl,
+                        DType t, hipStream_t s) {
+  if (M <= 0) return;
+  if (t == DType::F32) ce_kernel<float><<<M, 256, 0, s>>>(logits, tgt, V, pad, loss_row, (float*)dl);
+  else ce_kernel<bf16><<<M, 256, 0, s>>>(logits, tgt, V, pad, loss_row, (bf16*)dl);
+  CAPGEN_HIP(hipGetLastError());
+}
+
+__global__ void loss_finalize_kernel(const float* __restrict__ loss_row, int M, const float* count, int focal,
+                                     float* loss_out, float* grad_scale) {
+  __shared__ float sh[4];
+  float acc = 0.f;
+  for (int c = threadIdx.x; c < M; c += 256) acc += loss_row[c];
+  acc = block_sum(acc, sh);
+  if (threadIdx.x == 0) {
+    const float n = *count;
+    const float ce = acc / n;
+    if (focal) {  // loss.py:20-28 with gamma = 2
+      const float pt = expf(-ce);
+      const float om = 1.f - pt;
+      *loss_out = om * om * ce;
+      *grad_scale = (2.f * om * pt * ce + om * om) / n;
+    } else {
+      *loss_out = ce;
+      *grad_scale = 1.f / n;
+    }
+  }
+}
+void loss_finalize(const float* loss_row, int M, const float* count, int focal, float* loss_out, float* grad_scale,
+                   hipStream_t s) {
+  loss_finalize_kernel<<<1, 256, 0, s>>>(loss_row, M, count, focal, loss_out, grad_scale);
+  CAPGEN_HIP(hipGetLastError());
+}
+
+// ---- Adam ---------------------------------------------------------------------------
+__global__ void adam_prep_kernel(int64_t* step, float lr, float b1, float b2, float* scal) {
+  const int64_t t = ++(*step);
+  const double bc1 = 1.0 - pow((double)b1, (double)t);
+  const double bc2 = 1.0 - pow((double)b2, (double)t);
+  scal[0] = (float)(-(double)lr / bc1);  // value of addcdiv_ (= -step_size)
+  scal[1] = (float)sqrt(bc2);            // bias_correction2_sqrt
+}
+void adam_prepare(int64_t* step, float lr, float b1, float b2, float* scal, hipStream_t s) {
+  adam_prep_kernel<<<1, 1, 0, s>>>(step, lr, b1, b2, scal);
+  CAPGEN_HIP(hipGetLastError());
+}
+
+__device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, float b1c, float b2, float b2c,
+                                         float eps, float neg_step, float bc2s) {
+  m = m + b1c * (g - m);                      // exp_avg.lerp_(grad, 1 - beta1)
+  v = v * b2 + b2c * (g * g);                 // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
+  const float denom = sqrtf(v) / bc2s + eps;  // (exp_avg_sq.sqrt() / bc2_sqrt).add_(eps)
+  p = p + (neg_step * m) / denom;             // param.addcdiv_(exp_avg, denom, value=-step_size)
+}
+
+__global__ void __launch_bounds__(256) adam_kernel(float4* __restrict__ p, const float4* __restrict__ g,
+                                                   float4* __restrict__ m, float4* __restrict__ v, size_t n4,
+                                                   float b1, float b2, float eps, const float* __restrict__ scal,
+                                                   bf16* __restrict__ shadow, size_t n_shadow) {
+  const float neg_step = scal[0], bc2s = scal[1];
+  const float b1c = 1.f - b1, b2c = 1.f - b2;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
+    adam_one(pp.x, gg.x, mm.x, vv.x, b1c, b2, b2c, eps, neg_step, bc2s);
+    adam_one(pp.y, gg.y, mm.y, vv.y, b1c, b2, b2c, eps, neg_step, bc2s);
+    adam_one(pp.z, gg.z, mm.z, vv.z, b1c, b2, b2c, eps, neg_step, bc2s);
+    adam_one(pp.w, gg.w, mm.w, vv.w, b1c, b2, b2c, eps, neg_step, bc2s);
+    p[i] = pp;
+    m[i] = mm;
+    v[i] = vv;
+    if (shadow && 4 * i < n_shadow) {
+      typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+      bf16x4 o = {(bf16)pp.x, (bf16)pp.y, (bf16)pp.z, (bf16)pp.w};
+      *reinterpret_cast<bf16x4*>(shadow + 4 * i) = o;
+    }
+  }
+}
+void adam_update(float* p, const float* g, float* m, float* v, size_t n, float b1, float b2, float eps,
+                 const float* scal, bf16* shadow, size_t n_shadow, hipStream_t s) {
+  require(n % 4 == 0 && n_shadow % 4 == 0, "adam: arena size must be a multiple of 4");
+  size_t n4 = n / 4;
+  int grid = (int)std::min<size_t>((n4 + 255) / 256, 256 * 8);
+  adam_kernel<<<grid, 256, 0, s>>>((float4*)p, (const float4*)g, (float4*)m, (float4*)v, n4, b1, b2, eps, scal,
+                                   shadow, n_shadow);
+  CAPGEN_HIP(hipGetLastError());
+}
+
+__global__ void to_bf16_kernel(const float* __restrict__ src, bf16* __restrict__ dst, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = (bf16)src[i];
+}
+void to_bf16(const float* src, bf16* dst, size_t n, hipStream_t s) {
+  if (!n) return;
+  int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
+  to_bf16_kernel<<<grid, 256, 0, s>>>(src, dst, n);
+  CAPGEN_HIP(hipGetLastError());
+}
+
+// ---- greedy / beam helpers ---------------------------------------------------------
+__global__ void __launch_bounds__(256) argmax_softmax_kernel(const float* __restrict__ logits, int V,
+                                                             int64_t* ids_out, int64_t ids_ld, int col,
+                                                             int32_t* next_ids, int64_t next_ld) {
+  __shared__ float sh[4];
+  __shared__ float bv[4];
+  __shared__ int bi[4];
+  const int b = blockIdx.x;
+  const float* x = logits + (int64_t)b * V;
+  float mx = -INFINITY;
+  for (int c = threadIdx.x; c < V; c += 256) mx = fmaxf(mx, x[c]);
+  mx = block_max(mx, sh);
+  float se = 0.f;
+  for (int c = threadIdx.x; c < V; c += 256) se += expf(x[c] - mx);
+  se = block_sum(se, sh);
+  // argmax over the softmax probabilities, first index on ties (torch.argmax)
+  float best = -1.f;
+  int bidx = 0x7fffffff;
+  for (int c = threadIdx.x; c < V; c += 256) {
+    float p = expf(x[c] - mx) / se;
+    if (p > best) {
+      best = p;
+      bidx = c;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float ov = __shfl_xor(best, o, 64);
+    int oi = __shfl_xor(bidx, o, 64);
+    if (ov > best || (ov == best && oi < bidx)) {
+      best = ov;
+      bidx = oi;
+    }
+  }
+  if ((threadIdx.x & 63) == 0) {
+    bv[threadIdx.x >> 6] = best;
+    bi[threadIdx.x >> 6] = bidx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    best = bv[0];
+    bidx = bi[0];
+    for (int w = 1; w < 4; ++w)
+      if (bv[w] > best || (bv[w] == best && bi[w] < bidx)) {
+        best = bv[w];
+        bidx = bi[w];
+      }
+    ids_out[(int64_t)b * ids_ld + col] = bidx;
+    if (next_ids) next_ids[(int64_t)b * next_ld] = bidx;
+  }
+}
+void argmax_softmax(const float* logits, int B, int V, int64_t* ids_out, int64_t ids_ld, int col, int32_t* next_ids,
+                    int64_t next_ld, hipStream_t s) {
+  argmax_softmax_kernel<<<B, 256, 0, s>>>(logits, V, ids_out, ids_ld, col, next_ids, next_ld);
+  CAPGEN_HIP(hipGetLastError());
+}
+
+__global__ void __launch_bounds__(256) softmax_rows_kernel(const float* __restrict__ logits, int V,
+                                                           float* __restrict__ probs) {
+  __shared__ float sh[4];
+  const int b = blockIdx.x;
+  const float* x = logits + (int64_t)b * V;
+  float* y = probs + (int64_t)b * V;
+  float mx = -INFINITY;
+  for (int c = threadIdx.x; c < V; c += 256) mx = fmaxf(mx, x[c]);
+  mx = block_max(mx, sh);
+  float se = 0.f;
+  for (int c = threadIdx.x; c < V; c += 256) se += expf(x[c] - mx);
+  se = block_sum(se, sh);
+  for (int c = threadIdx.x; c < V; c += 256) y[c] = expf(x[c] - mx) / se;
+}
+void softmax_rows(const float* logits, int B, int V, float* probs, hipStream_t s) {
+  softmax_rows_kernel<<<B, 256, 0, s>>>(logits, V, probs);
+  CAPGEN_HIP(hipGetLastError());
+}
+
+__global__ void bump_seed_kernel(uint64_t* seed) { *seed += 0x9E3779B97F4A7C15ull; }
+void bump_seed(uint64_t* seed, hipStream_t s) {
+  bump_seed_kernel<<<1, 1, 0, s>>>(seed);
+  CAPGEN_HIP(hipGetLastError());
+}
+
+}  // namespace capgen

@@ -1,0 +1,136 @@
+/* capgen — C ABI of the MI355X-native caption-generator training engine (libcapgen.so).
+ *
+ * Drop-in boundary.  The reference has no FFI: its boundary is the
+ * Python object API of core/models.py (TRANSFORMER, models.py:81-135) over
+ * core/TRANSFORMER/model.py (Transformer, model.py:8-209).  Every entry point below
+ * replaces one reference call; the Python mirror (image-caption_amd/capgen) binds them
+ * with ctypes and keeps the reference method names, arguments and return types.
+ *
+ * Conventions: all functions return 0 on success, nonzero on failure, with a
+ * thread-local message from capgen_last_error().  Device pointers are plain pointers
+ * into the current HIP device's memory; `stream` is a hipStream_t passed as void*
+ * (NULL = default stream).  Calls on one handle are not thread-safe and are
+ * asynchronous on `stream` unless stated otherwise.  The library owns weights, grads,
+ * optimizer state and workspaces; the caller owns input/output buffers.
+ */
+#ifndef CAPGEN_H
+#define CAPGEN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CAPGEN_ABI_VERSION 1
+
+typedef struct capgen_engine capgen_t;
+
+enum capgen_dtype { CAPGEN_F32 = 0, CAPGEN_BF16 = 1 };
+
+/* Model/solver shape.  Field meanings follow Transformer.__init__ (model.py:10-36) and
+ * core/config.py:5-62; `max_length` is the Transformer's max_length (the decoder
+ * positional table has max_length-1 rows, model.py:383-396). */
+typedef struct capgen_config {
+  int32_t num_vocab, max_length;
+  int32_t dim_features, dim_positions;                 /* ENCODE_DIM_FEATURES / _POSITIONS */
+  int32_t enc_d, enc_ff, enc_blocks, enc_heads;        /* encode_input_size(=q_k=v), hidden, blocks, heads */
+  int32_t dim_word_embedding;
+  int32_t dec_d, dec_ff, dec_blocks, dec_heads;
+  float dropout;                                       /* DROPOUT (modules.py:64,106) */
+  float attention_dropout;                             /* 0.1, hard-coded at modules.py:8 */
+  int32_t pad_idx;                                     /* PAD_IDX */
+  int32_t encode_mask;                                 /* ENCODE_MASK (model.py:311-328) */
+  int32_t focal_loss;                                  /* 'FocalLoss' in OUTPUT_NAME (model.py:73-76) */
+  int32_t dtype;                                       /* capgen_dtype: compute/storage of activations */
+  int32_t max_batch, max_regions;                      /* workspace sizing hints */
+  float lr, beta1, beta2, eps;                         /* torch.optim.Adam (models.py:111-113) */
+  uint64_t seed;                                       /* dropout RNG seed */
+} capgen_config;
+
+/* One reference state_dict tensor mapped into the packed parameter arena:
+ * element (r, c) of the reference tensor lives at arena[offset + r*row_stride + c]. */
+typedef struct capgen_param_info {
+  char name[96];
+  int32_t ndim;
+  int64_t rows, cols;   /* 1-D tensors: rows = 1 */
+  int64_t offset, row_stride;
+} capgen_param_info;
+
+const char* capgen_last_error(void);
+int capgen_abi_version(void);
+
+/* Host-only (no device needed): the parameter table for a config.  Writes up to `cap`
+ * entries, sets *count to the total; *arena_elems = arena size in f32 elements. */
+int capgen_param_table(const capgen_config* cfg, capgen_param_info* out, int cap, int* count,
+                       int64_t* arena_elems);
+
+/* Transformer(...).to(DEVICE) + Adam(...)  — models.py:86-113. */
+int capgen_create(const capgen_config* cfg, int device, capgen_t** out);
+int capgen_destroy(capgen_t* h);
+
+/* state_dict()/load_state_dict() (models.py:62-68) go through these synchronous host
+ * copies of the whole f32 arena (layout: capgen_param_table). */
+int capgen_get_params(capgen_t* h, float* host_dst, int64_t n);
+int capgen_set_params(capgen_t* h, const float* host_src, int64_t n);  /* also resets nothing else */
+int capgen_get_grads(capgen_t* h, float* host_dst, int64_t n);
+/* Adam state: step count and exp_avg / exp_avg_sq arenas (optional checkpoint interop). */
+int capgen_get_adam_state(capgen_t* h, int64_t* step, float* exp_avg, float* exp_avg_sq, int64_t n);
+int capgen_set_adam_state(capgen_t* h, int64_t step, const float* exp_avg, const float* exp_avg_sq, int64_t n);
+/* Device pointers of the f32 parameter / gradient arenas (for zero-copy views). */
+int capgen_arenas(capgen_t* h, float** params, float** grads, int64_t* n);
+
+/* nn.Module.train()/eval(): dropout on/off (modules.py:12,64,106). */
+int capgen_set_training(capgen_t* h, int training);
+
+/* Transformer.forward (model.py:79-98) in training state: saves activations for
+ * capgen_backward.  feats [B,N,F] (feats_dtype), pos [B,N,P] f32, caps [B,T] int32, all
+ * device pointers.  loss_out: device f32 scalar (NULL = internal). */
+int capgen_forward(capgen_t* h, const void* feats, int feats_dtype, const float* pos, const int32_t* caps,
+                   int B, int N, int T, float* loss_out, void* stream);
+/* loss.backward() (models.py:125): fills the gradient arena (overwrites, = zero_grad + backward). */
+int capgen_backward(capgen_t* h, void* stream);
+/* optimizer.step() (models.py:126). */
+int capgen_adam_step(capgen_t* h, void* stream);
+/* TRANSFORMER.train_step (models.py:115-126): forward + backward (+ DP gradient
+ * all-reduce) + Adam, replayed from a captured hipGraph after the first call with a
+ * given (shape, pointers). */
+int capgen_train_step(capgen_t* h, const void* feats, int feats_dtype, const float* pos, const int32_t* caps,
+                      int B, int N, int T, float* loss_out, void* stream);
+int capgen_set_graph(capgen_t* h, int enable);
+/* TRANSFORMER.compute_loss (models.py:128-135): forward under no_grad. */
+int capgen_compute_loss(capgen_t* h, const void* feats, int feats_dtype, const float* pos, const int32_t* caps,
+                        int B, int N, int T, float* loss_out, void* stream);
+/* Logits of the last forward/compute_loss, [B*(T-1), V] f32 device copy (test hook). */
+int capgen_copy_logits(capgen_t* h, float* dst, int64_t n, void* stream);
+
+/* Transformer.generate_caption_vector (model.py:101-132): greedy decode, bit-identical
+ * to the reference's full-prefix recompute but KV-cached.  ids_out: [B, max_length+1]
+ * int64 device; attn_out (nullable): [max_length-1, B, N] f32 device (attention_list). */
+int capgen_greedy(capgen_t* h, const void* feats, int feats_dtype, const float* pos, int B, int N,
+                  int64_t* ids_out, float* attn_out, void* stream);
+/* Transformer.beam_search (model.py:135-200): ids_out [B, max_length] int64 device. */
+int capgen_beam(capgen_t* h, const void* feats, int feats_dtype, const float* pos, int B, int N, int beam_size,
+                int64_t* ids_out, void* stream);
+
+/* Reset the device-side dropout RNG state (test hook: replays a dropout mask). */
+int capgen_set_rng_seed(capgen_t* h, uint64_t seed);
+/* Kernel test hook: C[M,N] = alpha*opA.opB (+bias)(relu) (+C if beta) with the engine's GEMM.
+ * ta: A stored [K][M]; tb: B stored [K][N] (else [N][K]).  in/out dtypes: capgen_dtype. */
+int capgen_debug_gemm(int M, int N, int K, const void* A, int64_t lda, int ta, const void* B, int64_t ldb, int tb,
+                      void* C, int64_t ldc, int in_dtype, int out_dtype, const float* bias, float alpha, int beta,
+                      int relu, void* stream);
+
+/* Data parallel (one process per GPU, RCCL over xGMI).  Rank 0 creates the 128-byte
+ * unique id; the host broadcasts it (torch.distributed store) and every rank calls
+ * capgen_dp_init, which also broadcasts rank 0's parameters. */
+int capgen_dp_unique_id(char out[128]);
+int capgen_dp_init(capgen_t* h, const char id[128], int rank, int world);
+/* Override the global non-pad target count used by the CE mean (<= 0: all-reduce it). */
+int capgen_dp_set_global_count(capgen_t* h, float count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CAPGEN_H */

@@ -1,0 +1,71 @@
+"""CPU: the C-ABI library loads, exports every symbol include/capgen.h declares, and its
+host-only parameter table matches the reference state_dict (no device calls)."""
+import os
+import re
+
+import pytest
+
+from capgen import _lib, preset
+from capgen.params import reference_param_specs, num_params
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(REPO, "include", "capgen.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(capgen_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    declared = header_functions()
+    assert len(declared) >= 20
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert sorted(_lib.EXPORTED) == declared
+
+
+def test_abi_version():
+    assert _lib.load().capgen_abi_version() == _lib.ABI_VERSION
+
+
+@pytest.mark.parametrize("name", ["C1", "C2"])
+def test_param_table_matches_reference_specs(name):
+    cfg = preset(name)
+    table, total = _lib.param_table(cfg)
+    specs = reference_param_specs(cfg)
+    assert [t[0] for t in table] == [s[0] for s in specs]
+    covered = 0
+    spans = []
+    for (n, ndim, rows, cols, off, stride), (_, shape) in zip(table, specs):
+        assert ndim == len(shape)
+        assert (rows, cols) == (shape if ndim == 2 else (1, shape[0]))
+        assert stride >= cols
+        spans.append((off, off + (rows - 1) * stride + cols, n))
+        covered += rows * cols
+    assert covered == num_params(cfg)
+    assert covered == (55707408 if name == "C2" else 1272808)
+    # no two tensors overlap (interleaved strided tensors checked element-wise below)
+    occ = bytearray(total)
+    for (n, ndim, rows, cols, off, stride) in table:
+        for r in range(rows):
+            seg = occ[off + r * stride: off + r * stride + cols]
+            assert not any(seg), n
+            occ[off + r * stride: off + r * stride + cols] = b"\x01" * cols
+    assert max(s[1] for s in spans) <= total
+
+
+def test_bad_config_raises_loudly():
+    cfg = preset("C1", num_vocab=1001)
+    with pytest.raises(NotImplementedError):
+        _lib.param_table(cfg)
+    cfg = preset("C1", split_position=True)
+    with pytest.raises(NotImplementedError):
+        _lib.param_table(cfg)
+
+
+def test_engine_refuses_cpu_device():
+    from capgen.engine import Engine
+    with pytest.raises(RuntimeError):
+        Engine(preset("C1"), "cpu")

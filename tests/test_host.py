@@ -1,0 +1,108 @@
+"""CPU: host-side logic of the boundary (synthetic data, decode_captions, vocab loading,
+checkpoint mapping, DP exact-mean rule over gloo)."""
+import os
+import pickle
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from capgen import preset
+from capgen.params import fixture_state_dict, reference_init_state_dict, reference_param_specs, sinusoid_table
+from capgen.synthetic import synthetic_batch
+from capgen.utils import decode_captions, load_word_to_idx
+
+
+def test_synthetic_batch_structure():
+    f, p, c = synthetic_batch(64, 36, 2048, 84, 20, 10000, seed=0)
+    assert f.shape == (64, 36, 2048) and p.shape == (64, 36, 84) and c.shape == (64, 20)
+    assert (f >= 0).all()
+    pad = torch.count_nonzero(p, dim=2) == 0
+    assert pad.any() and not pad[:, 0].any()                # row 0 = whole image, never padding
+    assert (f[pad] == 0).all()                              # padded regions zero in both tensors
+    nv = (~pad).sum(1)
+    assert nv.min() >= 12 and nv.max() <= 36
+    assert (c[:, 0] == 1).all()
+    assert ((c == 2).sum(1) == 1).all()                     # exactly one <END>
+    assert (c[c > 2] >= 4).all()
+    f2, _, _ = synthetic_batch(64, 36, 2048, 84, 20, 10000, seed=0)
+    assert torch.equal(f, f2)
+
+
+def test_decode_captions_rules():
+    idx = {0: "<NULL>", 1: "<START>", 2: "<END>", 3: "a", 4: "cat", 5: "sits"}
+    caps = np.array([[1, 3, 4, 5, 2, 3, 0], [1, 3, 0, 4, 0, 0, 0]])
+    assert decode_captions(caps, idx) == ["a cat sits .", "a cat"]
+    assert decode_captions(np.array([1, 4, 2]), idx) == ["cat ."]
+
+
+def test_vocab_loader_accepts_data_pickle_and_refuses_code():
+    with tempfile.TemporaryDirectory() as d:
+        good = os.path.join(d, "word_index.pkl")
+        with open(good, "wb") as f:
+            pickle.dump({"<NULL>": 0, "<START>": 1, "<END>": 2}, f)
+        assert load_word_to_idx(good)["<END>"] == 2
+        bad = os.path.join(d, "evil.pkl")
+        with open(bad, "wb") as f:
+            pickle.dump(np.zeros(3), f)   # needs find_class -> refused
+        with pytest.raises(pickle.UnpicklingError):
+            load_word_to_idx(bad)
+
+
+def test_state_dict_specs_and_inits():
+    cfg = preset("C1")
+    for sd in (fixture_state_dict(cfg, 0), reference_init_state_dict(cfg, 0)):
+        names = [n for n, _ in reference_param_specs(cfg)] + ["decoder.position_embedding.pos_table"]
+        assert list(sd) == names
+        assert np.all(sd["decoder.word_embedding.weight"][0] == 0)
+        assert sd["decoder.position_embedding.pos_table"].shape == (1, cfg.max_length - 1, 128)
+    t = sinusoid_table(5, 8)
+    assert np.allclose(t[0, 0::2], 0) and np.allclose(t[0, 1::2], 1)
+
+
+def _dp_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from capgen.dp import global_target_count, local_target_count
+    from oracle import capgen_oracle as O
+    cfg = preset("C1")
+    f, p, c = synthetic_batch(8, 8, 512, 84, 10, 1000, seed=5, min_valid=4)
+    sl = slice(rank * 4, rank * 4 + 4)
+    P = O.make_params(fixture_state_dict(cfg, 0, with_buffer=False))
+    logits = O.forward_logits(P, cfg, f[sl], p[sl], c[sl], training=False)
+    tgt = c[sl].long()[:, 1:].reshape(-1)
+    summed = torch.nn.functional.cross_entropy(logits.reshape(-1, 1000), tgt, ignore_index=0, reduction="sum")
+    n_glob = global_target_count(c[sl])
+    (summed / n_glob).backward()            # exact-mean rule: local sum / GLOBAL count
+    g = torch.cat([v.grad.reshape(-1) for v in P.values()])
+    dist.all_reduce(g)
+    loss = torch.tensor([summed.item() / n_glob])
+    dist.all_reduce(loss)
+    if rank == 0:
+        out.put((loss.item(), g.numpy(), local_target_count(c[sl])))
+    dist.destroy_process_group()
+
+
+def test_dp_exact_mean_gloo_world2_matches_single_process():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    loss_dp, g_dp, _ = q.get(timeout=300)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    from oracle import capgen_oracle as O
+    cfg = preset("C1")
+    f, p, c = synthetic_batch(8, 8, 512, 84, 10, 1000, seed=5, min_valid=4)
+    P = O.make_params(fixture_state_dict(cfg, 0, with_buffer=False))
+    loss, _ = O.forward_loss(P, cfg, f, p, c, training=False)
+    loss.backward()
+    g = torch.cat([v.grad.reshape(-1) for v in P.values()]).numpy()
+    assert abs(loss.item() - loss_dp) < 1e-5
+    np.testing.assert_allclose(g_dp, g, atol=1e-6, rtol=1e-4)
