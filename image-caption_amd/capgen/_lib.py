@@ -66,6 +66,7 @@ _SIGS = {
     "capgen_set_rng_seed": (C.c_int, [_P, C.c_uint64]),
     "capgen_debug_gemm": (C.c_int, [C.c_int, C.c_int, C.c_int, _P, C.c_int64, C.c_int, _P, C.c_int64, C.c_int,
                                     _P, C.c_int64, C.c_int, C.c_int, _P, C.c_float, C.c_int, C.c_int, _P]),
+    "capgen_debug_gemm_variant": (C.c_int, [C.c_int]),
     "capgen_dp_unique_id": (C.c_int, [C.c_char_p]),
     "capgen_dp_init": (C.c_int, [_P, C.c_char_p, C.c_int, C.c_int]),
     "capgen_dp_set_global_count": (C.c_int, [_P, C.c_float]),

@@ -13,6 +13,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -206,6 +207,12 @@ struct capgen_engine {
              drop == o.drop;
     }
   } gkey{};
+  std::vector<std::array<int, 3>> tuned_shapes;
+  bool tuned(int B, int N, int T) const {
+    for (auto& t : tuned_shapes)
+      if (t[0] == B && t[1] == N && t[2] == T) return true;
+    return false;
+  }
   // data parallel
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
@@ -243,8 +250,9 @@ struct capgen_engine {
   }
   // dX[M,K] (+)= alpha * dY[M,N] . W[N,K]
   void linear_dx(const void* dY, int64_t ldy, int64_t woff, int64_t ldw, void* dX, int64_t ldx, int M, int N, int K,
-                 int beta, const void* relu_aux, const float* alpha_ptr, hipStream_t s) {
+                 int beta, const void* relu_aux, const float* alpha_ptr, hipStream_t s, float* colsum = nullptr) {
     GemmArgs ga;
+    ga.colsum = colsum;
     ga.M = M, ga.N = K, ga.K = N, ga.A = dY, ga.lda = ldy, ga.B = W(woff), ga.ldb = ldw, ga.C = dX, ga.ldc = ldx;
     ga.beta = beta;
     ga.aux = relu_aux;
@@ -498,12 +506,10 @@ struct capgen_engine {
                RowMask mask, Drop drop, void* r_out, hipStream_t s) {
     LnBwd lb;
     lb.M = M, lb.d = d, lb.dy = g_in, lb.v = v, lb.mean = mean, lb.rstd = rstd, lb.gamma = P(lng), lb.mask = mask;
-    lb.drop = drop, lb.d_res = r_out, lb.d_a = a.gA, lb.dgamma = G(lng), lb.dbeta = G(lnb);
+    lb.drop = drop, lb.d_res = r_out, lb.d_a = a.gA, lb.dgamma = G(lng), lb.dbeta = G(lnb), lb.dbias = G(b2);
     layernorm_bwd(lb, act, s);
-    column_sum(a.gA, M, d, d, 1.f, nullptr, G(b2), act, s);
     linear_dw(a.gA, d, H, f, W2, f, M, d, f, nullptr, s);
-    linear_dx(a.gA, d, W2, f, a.gH, f, M, d, f, 0, H, nullptr, s);  // x relu'(H)
-    column_sum(a.gH, M, f, f, 1.f, nullptr, G(b1), act, s);
+    linear_dx(a.gA, d, W2, f, a.gH, f, M, d, f, 0, H, nullptr, s, G(b1));  // x relu'(H); db1 = colsum
     linear_dw(a.gH, f, X, d, W1, d, M, f, d, nullptr, s);
     linear_dx(a.gH, f, W1, d, r_out, d, M, f, d, 1, nullptr, nullptr, s);
   }
@@ -659,6 +665,14 @@ struct capgen_engine {
     } else {
       if (!(gexec && gkey == k)) {
         drop_graph();
+        // one eager forward+backward (no all-reduce, no Adam) so every GEMM shape of the
+        // step is autotuned outside the capture; its gradients are overwritten below
+        if (!tuned(B, N, T)) {
+          forward(f, ft, pos, caps, B, N, T, loss, /*drop_on=*/false, es);  // no RNG advance
+          backward(es);
+          CAPGEN_HIP(hipStreamSynchronize(es));
+          tuned_shapes.push_back({B, N, T});
+        }
         hipGraph_t graph = nullptr;
         CAPGEN_HIP(hipStreamBeginCapture(es, hipStreamCaptureModeThreadLocal));
         try {
@@ -962,6 +976,7 @@ int capgen_create(const capgen_config* cfg, int device, capgen_t** out) {
     CAPGEN_HIP(hipGetDeviceCount(&ndev));
     require(device >= 0 && device < ndev, "capgen_create: invalid device index");
     CAPGEN_HIP(hipSetDevice(device));
+    gemm_init();
     auto h = std::make_unique<capgen_engine>();
     h->cfg = *cfg;
     h->L = make_layout(*cfg);
@@ -1178,11 +1193,16 @@ int capgen_debug_gemm(int M, int N, int K, const void* A, int64_t lda, int ta, c
                       void* Cp, int64_t ldc, int in_dtype, int out_dtype, const float* bias, float alpha, int beta,
                       int relu, void* stream) {
   return guarded([&] {
+    gemm_init();
     GemmArgs ga;
     ga.M = M, ga.N = N, ga.K = K, ga.A = A, ga.lda = lda, ga.B = B, ga.ldb = ldb, ga.C = Cp, ga.ldc = ldc;
     ga.bias = bias, ga.alpha = alpha, ga.beta = beta, ga.relu = relu;
     gemm(ga, dt(in_dtype), dt(out_dtype), ta != 0, tb != 0, (hipStream_t)stream);
   });
+}
+
+int capgen_debug_gemm_variant(int v) {
+  return guarded([&] { gemm_set_variant(v); });
 }
 
 int capgen_dp_unique_id(char out[128]) {

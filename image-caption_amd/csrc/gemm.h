@@ -23,9 +23,17 @@ struct GemmArgs {
   const float* alpha_ptr = nullptr;  // device scalar multiplied into alpha (e.g. 1/count)
   int beta = 0;                      // 1: accumulate into C
   int relu = 0;
+  float* colsum = nullptr;           // += column sums of the (post-epilogue, beta=0) output, f32 [N]
 };
 
 // ta: A stored [K][M] (else [M][K]); tb: B stored [K][N] (else [N][K]).
 void gemm(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t s);
+// allocate the per-device zero page used for out-of-range tiles (call before any bf16 gemm,
+// outside graph capture)
+void gemm_init();
+// experiment hook: force a bf16 GEMM tile/wave/stage variant (0 = heuristic)
+void gemm_set_variant(int v);
+// bf16-operand path (gemm_bf16.hip); called by gemm() after argument checks
+void gemm_bf16(const GemmArgs& g, DType out, bool ta, bool tb, hipStream_t s);
 
 }  // namespace capgen

@@ -1,4 +1,4 @@
-// capgen — MFMA GEMM for gfx950 with fused epilogues.
+// capgen — GEMM front end + the f32 parity-mode kernel (bf16 path: gemm_bf16.hip).
 //
 //   C[m][n] = epi( alpha * sum_k opA(m,k) * opB(k,n) )
 //   opA(m,k) = TA ? A[k*lda + m] : A[m*lda + k]
@@ -14,6 +14,7 @@
 // the current tile, write them to the other LDS buffer after).  Transposed operands are
 // transposed on the LDS write so every MFMA fragment is one 16-B ds_read (bf16).
 #include "gemm.h"
+#include "ops.h"
 
 namespace capgen {
 
@@ -217,12 +218,13 @@ void gemm(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t 
   require((tb ? g.N : g.K) % vec == 0 && g.ldb % vec == 0, "gemm: B contiguous dim/ld not a multiple of 16 B");
   require(((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0, "gemm: operands must be 16-B aligned");
   require(g.K > 0, "gemm: K must be positive");
+  require(!g.colsum || !g.beta, "gemm: colsum requires beta == 0");
   if (in == DType::F32) {
     if (out == DType::F32) launch_layout<float, float>(g, ta, tb, s);
     else launch_layout<float, bf16>(g, ta, tb, s);
+    if (g.colsum) column_sum(g.C, g.M, g.N, g.ldc, 1.f, nullptr, g.colsum, out, s);
   } else {
-    if (out == DType::F32) launch_layout<bf16, float>(g, ta, tb, s);
-    else launch_layout<bf16, bf16>(g, ta, tb, s);
+    gemm_bf16(g, out, ta, tb, s);
   }
   CAPGEN_HIP(hipGetLastError());
 }

@@ -1,0 +1,536 @@
+// capgen — bf16 MFMA GEMM for gfx950, all three training layouts in one kernel template.
+//
+//   NT (forward  X.W^T)    : A [M][K], B [N][K]   both K-contiguous
+//   NN (input grad dY.W)   : A [M][K], B [K][N]   B row-contiguous   (TB)
+//   TN (weight grad dY^T.X): A [K][M], B [K][N]   both row-contiguous (TA, TB)
+//
+// Data movement.  Every operand tile is moved HBM/L2 -> LDS by global_load_lds_dwordx4
+// (LDS-DMA, no staging registers) in its NATIVE layout, three stages deep: the DMA for
+// K-tile kt+2 is in flight while tile kt is multiplied, retired by a counted
+// `s_waitcnt vmcnt(loads per tile)` + raw s_barrier (never vmcnt(0) in the loop).
+// LDS-DMA writes lane-linearly, so the bank-conflict swizzles are applied to the
+// per-lane SOURCE address and undone on the fragment read (same involution).
+// Out-of-range rows / K columns read a device zero page (no OOB access, exact K tails).
+//
+// Fragments.  K-contiguous images (128-B rows) are read with two ds_read_b64, XOR-
+// swizzled in 16-B chunks by ((row>>1)&7).  Row-contiguous images are read with two
+// ds_read_b64_tr_b16 (CDNA4 LDS transpose read), XOR-swizzled per K row.  Within each
+// 32-deep v_mfma_f32_16x16x32_bf16 step, lane group g = lane>>4 carries k = 4g..4g+3
+// (elements 0-3) and 16+4g..16+4g+3 (elements 4-7) for BOTH operands — the same K
+// permutation on A and B leaves the dot product unchanged and makes every tr read of a
+// half-wave cover 8 consecutive K rows (conflict free).  NT, NN and TN therefore run at
+// the same LDS cost.
+//
+// Epilogue.  The MFMA is issued as B.A (operands swapped) so each lane ends with 4
+// CONSECUTIVE output columns of one row: bias/relu-mask/accumulate/convert are applied
+// on 4-wide vectors and stored as one 8-B (bf16) or 16-B (f32) write.
+//
+// Tiles BMxBNx64, 256 threads = 2x2 wave64s; blocks remapped so consecutive tiles (sharing
+// an A row-panel) land on the same XCD L2.
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <tuple>
+
+#include "gemm.h"
+
+namespace capgen {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef short s4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4 lds_s4;
+typedef __attribute__((address_space(3))) void lds_void;
+
+namespace {
+
+constexpr int BK = 64;
+
+void* g_zero_page[64] = {};
+
+// swizzles (16-B chunk index permutations, involutions)
+// [row][64 k]: key ((row>>1) ^ (row>>4)) & 7 is a bijection on any 16 aligned rows (conflict-free
+// ds_read_b64 fragments) AND differs between rows r and r+16, so hipcc cannot fuse two
+// fragments' reads into a ds_read2st64_b64 (mod-32 banking: 2-way conflicts)
+__device__ __forceinline__ int swz_k(int row, int chunk) { return chunk ^ (((row >> 1) ^ (row >> 4)) & 7); }
+template <int ROWS>
+__device__ __forceinline__ int swz_t(int k, int chunk) {                                   // [k][ROWS]
+  return ROWS == 128 ? chunk ^ ((k & 7) << 1) : chunk ^ (((k >> 1) & 3) << 1);
+}
+
+template <bool TRANS, int ROWS, int NW>
+struct Op {
+  static constexpr int BYTES = ROWS * BK * 2;   // one stage of this operand
+  static constexpr int NI = BYTES / 1024;       // 1-KB DMA instructions per stage
+  static constexpr int PER_WAVE = NI / NW;
+  static_assert(PER_WAVE >= 1 && NI % NW == 0, "tile too small for the wave count");
+
+  // issue this wave's share of the LDS-DMA for one K tile
+  static __device__ __forceinline__ void issue(const bf16* __restrict__ src, int64_t ld, int r0, int R, int k0,
+                                               int K, char* img, int wave, int lane, const void* zero) {
+#pragma unroll
+    for (int j = 0; j < PER_WAVE; ++j) {
+      const int i = wave + NW * j;
+      const int b = i * 1024 + lane * 16;
+      const bf16* p;
+      bool ok;
+      if constexpr (!TRANS) {
+        const int row = b >> 7, ch = swz_k(row, (b >> 4) & 7);
+        ok = (r0 + row < R) && (k0 + ch * 8 < K);
+        p = src + (int64_t)(r0 + row) * ld + (k0 + ch * 8);
+      } else {
+        const int k = b / (ROWS * 2), ch = swz_t<ROWS>(k, (b % (ROWS * 2)) >> 4);
+        ok = (k0 + k < K) && (r0 + ch * 8 < R);
+        p = src + (int64_t)(k0 + k) * ld + (r0 + ch * 8);
+      }
+      __builtin_amdgcn_global_load_lds(ok ? (const void*)p : zero, (lds_void*)(img + i * 1024), 16, 0, 0);
+    }
+  }
+
+  // 16-row fragment starting at rb for k-step ks (permuted K order, see header)
+  static __device__ __forceinline__ bf16x8 frag(const char* img, int rb, int ks, int lane) {
+    const int g = lane >> 4;
+    s4 lo, hi;
+    if constexpr (!TRANS) {
+      const int row = rb + (lane & 15);
+      const int c1 = ks * 4 + (g >> 1), sub = (g & 1) * 8;
+      lo = *reinterpret_cast<const s4*>(img + row * 128 + swz_k(row, c1) * 16 + sub);
+      hi = *reinterpret_cast<const s4*>(img + row * 128 + swz_k(row, c1 + 2) * 16 + sub);
+    } else {
+      const int i = lane & 15, q = i >> 2, p = i & 3;
+      const int k = ks * 32 + 4 * g + q;
+      const int ch = (rb >> 3) + (p >> 1), sub = (p & 1) * 8;
+      lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_s4*)(img + k * (ROWS * 2) + swz_t<ROWS>(k, ch) * 16 + sub));
+      hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_s4*)(img + (k + 16) * (ROWS * 2) + swz_t<ROWS>(k + 16, ch) * 16 + sub));
+    }
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  }
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <typename TO>
+__device__ __forceinline__ void load4(const TO* p, float (&v)[4]) {
+  if constexpr (sizeof(TO) == 4) {
+    float4 x = *reinterpret_cast<const float4*>(p);
+    v[0] = x.x, v[1] = x.y, v[2] = x.z, v[3] = x.w;
+  } else {
+    typedef __attribute__((ext_vector_type(4))) __bf16 b4;
+    b4 x = *reinterpret_cast<const b4*>(p);
+    v[0] = (float)x[0], v[1] = (float)x[1], v[2] = (float)x[2], v[3] = (float)x[3];
+  }
+}
+template <typename TO>
+__device__ __forceinline__ void store4(TO* p, const float (&v)[4]) {
+  if constexpr (sizeof(TO) == 4) {
+    *reinterpret_cast<float4*>(p) = float4{v[0], v[1], v[2], v[3]};
+  } else {
+    typedef __attribute__((ext_vector_type(4))) __bf16 b4;
+    *reinterpret_cast<b4*>(p) = b4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+  }
+}
+
+}  // namespace
+
+template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int STAGES>
+__global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmArgs g, int tiles_n, int nblk,
+                                                                const void* zero, int splitk, float* ws) {
+  constexpr int NW = WM * WN;
+  typedef Op<TA, BM, NW> OA;
+  typedef Op<TB, BN, NW> OB;
+  constexpr int SB = OA::BYTES + OB::BYTES;         // bytes per stage
+  constexpr int LPT = OA::PER_WAVE + OB::PER_WAVE;  // DMA instructions per wave per K tile
+  constexpr int TM = BM / WM, TN = BN / WN;         // per-wave tile
+  constexpr int FM = TM / 16, FN = TN / 16;
+  static_assert(STAGES >= 2, "need >= 2 stages");
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * SB];
+
+  // XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> give them adjacent tiles
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  const int slot = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tile = slot / splitk, split = slot % splitk;  // split-K slices of a tile are adjacent
+  const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
+
+  const bf16* __restrict__ A = reinterpret_cast<const bf16*>(g.A);
+  const bf16* __restrict__ B = reinterpret_cast<const bf16*>(g.B);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk_all = (g.K + BK - 1) / BK;
+  const int per = (nk_all + splitk - 1) / splitk;
+  const int kt0 = split * per;
+  const int nk = max(0, min(nk_all - kt0, per));  // K tiles of this slice
+  auto issue = [&](int kt) {
+    kt += kt0;
+    char* st = smem + ((kt - kt0) % STAGES) * SB;
+    OA::issue(A, g.lda, m0, g.M, kt * BK, g.K, st, wave, lane, zero);
+    OB::issue(B, g.ldb, n0, g.N, kt * BK, g.K, st + OA::BYTES, wave, lane, zero);
+  };
+#pragma unroll
+  for (int p = 0; p < STAGES - 1; ++p)
+    if (p < nk) issue(p);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    // tile kt landed for this wave (up to STAGES-2 younger tiles may still fly) ...
+    const int younger = min(STAGES - 2, nk - 1 - kt);
+    if constexpr (STAGES >= 4) {
+      if (younger >= 2) wait_vmcnt<2 * LPT>();
+      else if (younger == 1) wait_vmcnt<LPT>();
+      else wait_vmcnt<0>();
+    } else if constexpr (STAGES == 3) {
+      if (younger >= 1) wait_vmcnt<LPT>();
+      else wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();  // ... for every wave; stage (kt-1)%STAGES is free again
+    if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1);
+    const char* st = smem + (kt % STAGES) * SB;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = OA::frag(st, wm * TM + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = OB::frag(st + OA::BYTES, wn * TN + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue: lane holds C[m = mb + (lane&15)][n = nb + 4*(lane>>4) + 0..3] ----
+  const float alpha = g.alpha_ptr ? g.alpha * *g.alpha_ptr : g.alpha;
+  if (splitk > 1) {  // partial sums -> f32 workspace; gemm_splitk_finalize applies the epilogue
+    const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wn * TN + j * 16 + fq * 4;
+      if (n >= g.N) continue;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int m = m0 + wm * TM + i * 16 + fr;
+        if (m >= g.M) continue;
+        float* w = ws + (int64_t)m * g.N + n;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) atomicAdd(w + r, alpha * acc[i][j][r]);
+      }
+    }
+    return;
+  }
+  TO* __restrict__ C = reinterpret_cast<TO*>(g.C);
+  const bf16* __restrict__ aux = reinterpret_cast<const bf16*>(g.aux);
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wn * TN + j * 16 + fq * 4;
+    float cs[4] = {0.f, 0.f, 0.f, 0.f};
+    if (n >= g.N) continue;
+    float bn[4] = {0.f, 0.f, 0.f, 0.f};
+    if (g.bias) {
+      float4 b4 = *reinterpret_cast<const float4*>(g.bias + n);
+      bn[0] = b4.x, bn[1] = b4.y, bn[2] = b4.z, bn[3] = b4.w;
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = m0 + wm * TM + i * 16 + fr;
+      if (m >= g.M) continue;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = alpha * acc[i][j][r] + bn[r];
+      if (aux) {
+        float a4[4];
+        load4<bf16>(aux + (int64_t)m * g.ldaux + n, a4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = a4[r] > 0.f ? v[r] : 0.f;
+      }
+      if (g.relu) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      TO* cp = C + (int64_t)m * g.ldc + n;
+      if (g.beta) {
+        float o[4];
+        load4<TO>(cp, o);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += o[r];
+      }
+      store4<TO>(cp, v);
+      if (g.colsum) {  // column sums of the stored values (as rounded to TO), from registers
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cs[r] += (float)(TO)v[r];
+      }
+    }
+    if (g.colsum) {
+      // reduce over the 16 lanes (rows) sharing these 4 columns, one atomic per column
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cs[r] += __shfl_xor(cs[r], o, 64);
+      if (fr == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) atomicAdd(g.colsum + n + r, cs[r]);
+      }
+    }
+  }
+}
+
+// split-K epilogue: C = epi(ws) over 64x64 tiles; colsum reduced per workgroup through LDS
+template <typename TO>
+__global__ void __launch_bounds__(256) gemm_splitk_finalize(GemmArgs g, const float* __restrict__ ws) {
+  __shared__ float red[16][65];
+  const int cg = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int n = blockIdx.x * 64 + cg * 4;
+  const bf16* __restrict__ aux = reinterpret_cast<const bf16*>(g.aux);
+  TO* __restrict__ C = reinterpret_cast<TO*>(g.C);
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  if (n < g.N) {
+    float bn[4] = {0.f, 0.f, 0.f, 0.f};
+    if (g.bias) {
+      float4 b4 = *reinterpret_cast<const float4*>(g.bias + n);
+      bn[0] = b4.x, bn[1] = b4.y, bn[2] = b4.z, bn[3] = b4.w;
+    }
+    for (int j = 0; j < 4; ++j) {
+      const int m = blockIdx.y * 64 + rl + 16 * j;
+      if (m >= g.M) break;
+      float4 w4 = *reinterpret_cast<const float4*>(ws + (int64_t)m * g.N + n);
+      float v[4] = {w4.x + bn[0], w4.y + bn[1], w4.z + bn[2], w4.w + bn[3]};
+      if (aux) {
+        float a4[4];
+        load4<bf16>(aux + (int64_t)m * g.ldaux + n, a4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = a4[r] > 0.f ? v[r] : 0.f;
+      }
+      if (g.relu) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      TO* cp = C + (int64_t)m * g.ldc + n;
+      if (g.beta) {
+        float o[4];
+        load4<TO>(cp, o);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += o[r];
+      }
+      store4<TO>(cp, v);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cs[r] += (float)(TO)v[r];
+    }
+  }
+  if (!g.colsum) return;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[rl][cg * 4 + r] = cs[r];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    if (c < g.N) {
+      float sum = 0.f;
+      for (int r = 0; r < 16; ++r) sum += red[r][threadIdx.x];
+      atomicAdd(g.colsum + c, sum);
+    }
+  }
+}
+
+struct Workspace {
+  float* p = nullptr;
+  size_t bytes = 0;
+};
+Workspace g_ws[64];
+
+// make sure the split-K workspace holds `bytes` (never called inside a stream capture)
+void ensure_ws(int dev, size_t bytes) {
+  if (g_ws[dev].bytes >= bytes) return;
+  if (g_ws[dev].p) CAPGEN_HIP(hipFree(g_ws[dev].p));
+  CAPGEN_HIP(hipMalloc(&g_ws[dev].p, bytes));
+  g_ws[dev].bytes = bytes;
+}
+
+template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int ST>
+static void launch_cfg(const GemmArgs& g, hipStream_t s, int splitk) {
+  const int tn = (g.N + BN - 1) / BN, tm = (g.M + BM - 1) / BM;
+  const int nblk = tn * tm * splitk;
+  int dev = 0;
+  CAPGEN_HIP(hipGetDevice(&dev));
+  float* ws = nullptr;
+  if (splitk > 1) {
+    const size_t bytes = (size_t)g.M * g.N * sizeof(float);
+    require(g_ws[dev].bytes >= bytes, "gemm: split-K workspace too small (tune outside capture)");
+    ws = g_ws[dev].p;
+    CAPGEN_HIP(hipMemsetAsync(ws, 0, bytes, s));
+  }
+  gemm_bf16_kernel<TO, TA, TB, BM, BN, WM, WN, ST>
+      <<<nblk, 64 * WM * WN, 0, s>>>(g, tn, nblk, g_zero_page[dev], splitk, ws);
+  if (splitk > 1) {
+    dim3 grid((g.N + 63) / 64, (g.M + 63) / 64);
+    gemm_splitk_finalize<TO><<<grid, 256, 0, s>>>(g, ws);
+  }
+}
+
+int g_variant = 0;  // experiment selector (capgen_debug_gemm_variant); 0 = tuned/heuristic
+
+// Tile / wave-grid / pipeline-depth variants.  Every variant accumulates the same K tiles
+// in the same order with the same MFMA sequence, so results are bit-identical across
+// variants: the choice is a pure speed decision (made per shape by the autotuner).
+constexpr int NVARIANTS = 11;
+const char* kVariantName[NVARIANTS + 1] = {"auto",        "128x128w4s3", "128x128w8s2", "128x128w4s2",
+                                           "128x64w4s2",  "64x128w4s2",  "64x64w4s2",   "64x64w4s3",
+                                           "128x64w8s2",  "256x128w16s2", "128x128w16s2", "256x64w8s2"};
+
+template <typename TO, bool TA, bool TB>
+static void launch_variant(int v, const GemmArgs& g, hipStream_t s, int sk = 1) {
+  switch (v) {
+    case 1: return launch_cfg<TO, TA, TB, 128, 128, 2, 2, 3>(g, s, sk);
+    case 2: return launch_cfg<TO, TA, TB, 128, 128, 2, 4, 2>(g, s, sk);
+    case 3: return launch_cfg<TO, TA, TB, 128, 128, 2, 2, 2>(g, s, sk);
+    case 4: return launch_cfg<TO, TA, TB, 128, 64, 2, 2, 2>(g, s, sk);
+    case 5: return launch_cfg<TO, TA, TB, 64, 128, 2, 2, 2>(g, s, sk);
+    case 6: return launch_cfg<TO, TA, TB, 64, 64, 2, 2, 2>(g, s, sk);
+    case 7: return launch_cfg<TO, TA, TB, 64, 64, 2, 2, 3>(g, s, sk);
+    case 8: return launch_cfg<TO, TA, TB, 128, 64, 4, 2, 2>(g, s, sk);
+    case 9: return launch_cfg<TO, TA, TB, 256, 128, 4, 4, 2>(g, s, sk);
+    case 10: return launch_cfg<TO, TA, TB, 128, 128, 4, 4, 2>(g, s, sk);
+    case 11: return launch_cfg<TO, TA, TB, 256, 64, 4, 2, 2>(g, s, sk);
+    default: throw Error("gemm: unknown variant");
+  }
+}
+
+int heuristic_variant(const GemmArgs& g) {
+  const long b64 = (long)((g.M + 63) / 64) * ((g.N + 63) / 64);
+  return b64 <= 4096 ? 6 : 3;
+}
+
+struct TuneKey {
+  int M, N, K, ta, tb, out;
+  bool operator<(const TuneKey& o) const {
+    return std::tie(M, N, K, ta, tb, out) < std::tie(o.M, o.N, o.K, o.ta, o.tb, o.out);
+  }
+};
+struct Choice {
+  int variant, splitk;
+};
+std::map<TuneKey, Choice> g_tuned;
+std::mutex g_tune_mu;
+
+bool autotune_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("CAPGEN_AUTOTUNE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+template <typename TO, bool TA, bool TB>
+static Choice tune(const GemmArgs& g, hipStream_t s) {
+  // time every (variant, split-K) on a scratch output (inputs untouched, beta forced to 0)
+  int dev = 0;
+  CAPGEN_HIP(hipGetDevice(&dev));
+  GemmArgs t = g;
+  void* scratch = nullptr;
+  CAPGEN_HIP(hipMalloc(&scratch, (size_t)g.M * g.ldc * sizeof(TO)));
+  t.C = scratch;
+  t.beta = 0;
+  t.colsum = nullptr;
+  hipEvent_t e0, e1;
+  CAPGEN_HIP(hipEventCreate(&e0));
+  CAPGEN_HIP(hipEventCreate(&e1));
+  Choice best{heuristic_variant(g), 1};
+  float best_ms = 1e30f;
+  const int nk = (g.K + BK - 1) / BK;
+  for (int sk : {1, 2, 4, 8}) {
+    if (sk > 1 && nk < 4 * sk) break;
+    if (sk > 1) ensure_ws(dev, (size_t)g.M * g.N * sizeof(float));
+    for (int v = 1; v <= NVARIANTS; ++v) {
+      launch_variant<TO, TA, TB>(v, t, s, sk);  // warm-up
+      CAPGEN_HIP(hipEventRecord(e0, s));
+      for (int r = 0; r < 3; ++r) launch_variant<TO, TA, TB>(v, t, s, sk);
+      CAPGEN_HIP(hipEventRecord(e1, s));
+      CAPGEN_HIP(hipEventSynchronize(e1));
+      float ms = 0.f;
+      CAPGEN_HIP(hipEventElapsedTime(&ms, e0, e1));
+      if (ms < best_ms) best_ms = ms, best = Choice{v, sk};
+    }
+  }
+  CAPGEN_HIP(hipEventDestroy(e0));
+  CAPGEN_HIP(hipEventDestroy(e1));
+  CAPGEN_HIP(hipFree(scratch));
+  if (std::getenv("CAPGEN_AUTOTUNE_LOG"))
+    std::fprintf(stderr, "[capgen gemm] M=%d N=%d K=%d ta=%d tb=%d out=%s -> %s splitk=%d (%.2f us)\n", g.M, g.N, g.K,
+                 TA, TB, sizeof(TO) == 4 ? "f32" : "bf16", kVariantName[best.variant], best.splitk,
+                 best_ms * 1e3f / 3);
+  return best;
+}
+
+template <typename TO, bool TA, bool TB>
+static void launch_bf16_tiles(const GemmArgs& g, hipStream_t s) {
+  Choice c{g_variant % 100, std::max(1, g_variant / 100)};  // forced: variant + 100 * splitk
+  if (c.splitk > 1) {
+    int dev = 0;
+    CAPGEN_HIP(hipGetDevice(&dev));
+    ensure_ws(dev, (size_t)g.M * g.N * sizeof(float));
+  }
+  if (c.variant == 0) {
+    c.variant = heuristic_variant(g);
+    if (autotune_enabled()) {
+      TuneKey key{g.M, g.N, g.K, TA, TB, (int)sizeof(TO)};
+      std::lock_guard<std::mutex> lk(g_tune_mu);
+      auto it = g_tuned.find(key);
+      if (it != g_tuned.end()) {
+        c = it->second;
+      } else {
+        hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+        CAPGEN_HIP(hipStreamIsCapturing(s, &st));
+        if (st == hipStreamCaptureStatusNone) c = g_tuned[key] = tune<TO, TA, TB>(g, s);
+      }
+    }
+  }
+  launch_variant<TO, TA, TB>(c.variant, g, s, c.splitk);
+}
+
+template <typename TO>
+static void launch_bf16_layout(const GemmArgs& g, bool ta, bool tb, hipStream_t s) {
+  if (!ta && !tb) launch_bf16_tiles<TO, false, false>(g, s);
+  else if (!ta && tb) launch_bf16_tiles<TO, false, true>(g, s);
+  else if (ta && !tb) launch_bf16_tiles<TO, true, false>(g, s);
+  else launch_bf16_tiles<TO, true, true>(g, s);
+}
+
+void gemm_set_variant(int v) { g_variant = v; }
+
+void gemm_init() {
+  int dev = 0;
+  CAPGEN_HIP(hipGetDevice(&dev));
+  require(dev >= 0 && dev < 64, "gemm_init: device index out of range");
+  if (!g_zero_page[dev]) {
+    CAPGEN_HIP(hipMalloc(&g_zero_page[dev], 4096));
+    CAPGEN_HIP(hipMemset(g_zero_page[dev], 0, 4096));
+  }
+}
+
+void gemm_bf16(const GemmArgs& g, DType out, bool ta, bool tb, hipStream_t s) {
+  int dev = 0;
+  CAPGEN_HIP(hipGetDevice(&dev));
+  require(g_zero_page[dev] != nullptr, "gemm: gemm_init() not called on this device");
+  require(g.N % 4 == 0 && g.ldc % 4 == 0 && (g.aux == nullptr || g.ldaux % 4 == 0),
+          "gemm(bf16): N/ldc must be multiples of 4");
+  if (out == DType::F32) launch_bf16_layout<float>(g, ta, tb, s);
+  else launch_bf16_layout<bf16>(g, ta, tb, s);
+}
+
+}  // namespace capgen

@@ -47,6 +47,7 @@ struct LnBwd {
   void* d_a = nullptr;     // grad wrt a (dropout mask applied), or null
   float* dgamma = nullptr;  // accumulated
   float* dbeta = nullptr;   // accumulated
+  float* dbias = nullptr;   // accumulated column sum of d_a (bias of the producing Linear), or null
 };
 void layernorm_bwd(const LnBwd& a, DType t, hipStream_t s);
 

@@ -75,12 +75,12 @@ __global__ void __launch_bounds__(LN_THREADS) ln_fwd_kernel(LnFwd a) {
 
 template <typename T, int DPL>
 __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(LnBwd a) {
-  __shared__ float red[2][LN_THREADS / 64][64 * DPL];
+  __shared__ float red[3][LN_THREADS / 64][64 * DPL];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int d = a.d, c0 = lane * DPL;
-  float dg[DPL], db[DPL];
+  float dg[DPL], db[DPL], dz[DPL];
 #pragma unroll
-  for (int e = 0; e < DPL; ++e) dg[e] = db[e] = 0.f;
+  for (int e = 0; e < DPL; ++e) dg[e] = db[e] = dz[e] = 0.f;
   const uint64_t seed = a.drop.seed_ptr ? *a.drop.seed_ptr : 0;
   for (int m = blockIdx.x * (LN_THREADS / 64) + wave; m < a.M; m += gridDim.x * (LN_THREADS / 64)) {
     const int64_t base = (int64_t)m * d + c0;
@@ -112,24 +112,31 @@ __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(LnBwd a) {
           dv[e] = drop_keep(seed, a.drop.site, (uint32_t)(base + e), a.drop.thresh) ? dv[e] * a.drop.scale : 0.f;
       }
       store_f<T, DPL>(reinterpret_cast<T*>(a.d_a) + base, dv);
+#pragma unroll
+      for (int e = 0; e < DPL; ++e) dz[e] += dv[e];
     }
   }
-  if (!a.dgamma) return;
+  if (!a.dgamma && !a.dbias) return;
 #pragma unroll
   for (int e = 0; e < DPL; ++e) {
     red[0][wave][c0 + e] = dg[e];
     red[1][wave][c0 + e] = db[e];
+    red[2][wave][c0 + e] = dz[e];
   }
   __syncthreads();
   for (int c = threadIdx.x; c < d; c += LN_THREADS) {
-    float sg = 0.f, sb = 0.f;
+    float sg = 0.f, sb = 0.f, sz = 0.f;
 #pragma unroll
     for (int w = 0; w < LN_THREADS / 64; ++w) {
       sg += red[0][w][c];
       sb += red[1][w][c];
+      sz += red[2][w][c];
     }
-    atomicAdd(a.dgamma + c, sg);
-    atomicAdd(a.dbeta + c, sb);
+    if (a.dgamma) {
+      atomicAdd(a.dgamma + c, sg);
+      atomicAdd(a.dbeta + c, sb);
+    }
+    if (a.dbias) atomicAdd(a.dbias + c, sz);
   }
 }
 
@@ -154,8 +161,8 @@ void layernorm_fwd(const LnFwd& a, DType t, hipStream_t s) {
 
 template <typename T>
 static void ln_bwd_dispatch(const LnBwd& a, hipStream_t s) {
-  const int rows_per_block = 32;  // 8 rows per wave -> fewer dgamma atomics
-  dim3 grid((a.M + rows_per_block - 1) / rows_per_block);
+  // ~256 workgroups: enough waves to cover the chip, few enough dgamma/dbeta atomics
+  dim3 grid(std::min(256, (a.M + 3) / 4));
   switch (a.d / 64) {
     case 1: ln_bwd_kernel<T, 1><<<grid, LN_THREADS, 0, s>>>(a); break;
     case 2: ln_bwd_kernel<T, 2><<<grid, LN_THREADS, 0, s>>>(a); break;
@@ -277,20 +284,51 @@ void embedding_scatter_add(const void* dE, const int32_t* ids, int M, int d, int
   CAPGEN_HIP(hipGetLastError());
 }
 
+// db[n] += alpha * sum_m X[m][n]: 16-B loads (a workgroup covers 8 vectors x 32 row lanes x
+// 8 rows per lane), rows reduced through LDS, one atomic per column per workgroup
 template <typename T>
-__global__ void colsum_kernel(const T* __restrict__ X, int M, int N, int64_t ldx, float alpha,
-                              const float* alpha_ptr, float* __restrict__ db) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  float acc = 0.f;
-  for (int m = blockIdx.y; m < M; m += gridDim.y) acc += to_f(X[(int64_t)m * ldx + n]);
-  const float a = alpha_ptr ? alpha * *alpha_ptr : alpha;
-  atomicAdd(db + n, a * acc);
+__global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ X, int M, int N, int64_t ldx, float alpha,
+                                                     const float* alpha_ptr, float* __restrict__ db) {
+  constexpr int V = 16 / sizeof(T);
+  __shared__ float red[32][8 * V + 1];
+  const int cv = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int n = (blockIdx.x * 8 + cv) * V;
+  float acc[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) acc[e] = 0.f;
+  if (n < N) {
+    const int r0 = blockIdx.y * 256;
+#pragma unroll 4
+    for (int j = 0; j < 8; ++j) {
+      const int m = r0 + rl + 32 * j;
+      if (m < M) {
+        float x[V];
+        load_f<T, V>(X + (int64_t)m * ldx + n, x);
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[e] += x[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < V; ++e) red[rl][cv * V + e] = acc[e];
+  __syncthreads();
+  if (threadIdx.x < 8 * V) {
+    const int c = threadIdx.x;
+    const int nn = blockIdx.x * 8 * V + c;
+    if (nn < N) {
+      float sum = 0.f;
+      for (int r = 0; r < 32; ++r) sum += red[r][c];
+      const float a = alpha_ptr ? alpha * *alpha_ptr : alpha;
+      atomicAdd(db + nn, a * sum);
+    }
+  }
 }
 void column_sum(const void* X, int M, int N, int64_t ldx, float alpha, const float* alpha_ptr, float* db, DType t,
                 hipStream_t s) {
   if (M <= 0 || N <= 0) return;
-  dim3 grid((N + 255) / 256, std::min(32, (M + 31) / 32));
+  const int V = t == DType::F32 ? 4 : 8;
+  require(N % V == 0 && ldx % V == 0, "column_sum: N/ld must be multiples of 16 B");
+  dim3 grid((N + 8 * V - 1) / (8 * V), (M + 255) / 256);
   if (t == DType::F32) colsum_kernel<float><<<grid, 256, 0, s>>>((const float*)X, M, N, ldx, alpha, alpha_ptr, db);
   else colsum_kernel<bf16><<<grid, 256, 0, s>>>((const bf16*)X, M, N, ldx, alpha, alpha_ptr, db);
   CAPGEN_HIP(hipGetLastError());

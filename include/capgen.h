@@ -122,6 +122,9 @@ int capgen_debug_gemm(int M, int N, int K, const void* A, int64_t lda, int ta, c
                       void* C, int64_t ldc, int in_dtype, int out_dtype, const float* bias, float alpha, int beta,
                       int relu, void* stream);
 
+/* Experiment hook: force a GEMM tile/wave/pipeline variant (0 = production heuristic). */
+int capgen_debug_gemm_variant(int variant);
+
 /* Data parallel (one process per GPU, RCCL over xGMI).  Rank 0 creates the 128-byte
  * unique id; the host broadcasts it (torch.distributed store) and every rank calls
  * capgen_dp_init, which also broadcasts rank 0's parameters. */

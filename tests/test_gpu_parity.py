@@ -199,3 +199,32 @@ def test_gemm_kernel_vs_torch(in_dt, ta, tb, M, N, K):
     torch.cuda.synchronize()
     tol = 1e-4 * np.sqrt(K) if in_dt == "fp32" else 2e-3 * np.sqrt(K)
     assert (Cd.cpu() - ref).abs().max().item() <= tol
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 206, 403, 810])
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 1)])
+def test_gemm_every_variant_and_splitk(variant, ta, tb):
+    """Each tile/wave/stage variant (and split-K factor: variant + 100*splitk) computes the
+    same product, M/N/K tails included."""
+    import ctypes as C
+    from capgen import _lib
+    lib = _lib.load()
+    M, N, K = 200, 264, 1000
+    g = torch.Generator(device="cpu").manual_seed(variant)
+    A = torch.randn(M, K, generator=g).bfloat16()
+    Bm = torch.randn(N, K, generator=g).bfloat16()
+    bias = torch.randn(N, generator=g)
+    ref = A.float() @ Bm.float().t() + bias
+    Ad = (A.t().contiguous() if ta else A).to(DEV)
+    Bd = (Bm.t().contiguous() if tb else Bm).to(DEV)
+    Cd = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    bd = bias.to(DEV)
+    _lib.check(lib.capgen_debug_gemm_variant(variant))
+    try:
+        _lib.check(lib.capgen_debug_gemm(M, N, K, C.c_void_p(Ad.data_ptr()), M if ta else K, ta,
+                                         C.c_void_p(Bd.data_ptr()), N if tb else K, tb, C.c_void_p(Cd.data_ptr()),
+                                         N, 1, 0, C.c_void_p(bd.data_ptr()), 1.0, 0, 0, None))
+        torch.cuda.synchronize()
+    finally:
+        _lib.check(lib.capgen_debug_gemm_variant(0))
+    assert (Cd.cpu() - ref).abs().max().item() <= 2e-3 * np.sqrt(K)

@@ -1,0 +1,77 @@
+"""GEMM microbenchmark via the capgen_debug_gemm test hook (run under rocprofv3 for
+exact per-dispatch durations, or standalone for event timing)."""
+import ctypes as C
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "image-caption_amd"))
+import torch  # noqa: E402
+
+from capgen import _lib  # noqa: E402
+
+lib = _lib.load()
+
+
+def run(M, N, K, ta=0, tb=0, out_f32=False, reps=20, bias=False, relu=False):
+    A = torch.randn((K, M) if ta else (M, K), device="cuda", dtype=torch.bfloat16)
+    B = torch.randn((K, N) if tb else (N, K), device="cuda", dtype=torch.bfloat16)
+    Cc = torch.empty(M, N, device="cuda", dtype=torch.float32 if out_f32 else torch.bfloat16)
+    b = torch.zeros(N, device="cuda")
+    def args():
+        s = torch.cuda.current_stream()
+        return (M, N, K, C.c_void_p(A.data_ptr()), M if ta else K, ta, C.c_void_p(B.data_ptr()), N if tb else K, tb,
+                C.c_void_p(Cc.data_ptr()), N, 1, 0 if out_f32 else 1, C.c_void_p(b.data_ptr()) if bias else None,
+                1.0, 0, int(relu), C.c_void_p(s.cuda_stream))
+    g = torch.cuda.CUDAGraph()
+    _lib.check(lib.capgen_debug_gemm(*args()))
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            _lib.check(lib.capgen_debug_gemm(*args()))
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    g.replay()
+    e1.record()
+    e1.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    tf = 2 * M * N * K / (us * 1e-6) / 1e12
+    print(f"M={M:6d} N={N:6d} K={K:6d} ta={ta} tb={tb} f32={int(out_f32)}  {us:8.2f} us  {tf:7.1f} TF/s", flush=True)
+    return us
+
+
+def sweep():
+    shapes = [(2304, 2048, 512, 0, 0, 0), (4096, 4096, 4096, 0, 0, 0), (2304, 6144, 512, 0, 0, 0),
+              (2048, 512, 2304, 1, 1, 1), (2304, 512, 2048, 0, 1, 0), (1216, 512, 512, 0, 1, 0)]
+    for v in range(0, 10):
+        _lib.check(lib.capgen_debug_gemm_variant(v))
+        print(f"--- variant {v}")
+        for sh in shapes:
+            try:
+                run(*sh)
+            except RuntimeError as e:
+                print("  skip", e)
+    _lib.check(lib.capgen_debug_gemm_variant(0))
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "lat":
+    for (M, N, K, v) in [(64, 64, 64, 6), (64, 64, 4096, 6), (64, 64, 4096, 7), (128, 128, 4096, 3),
+                         (128, 128, 4096, 1), (256, 128, 4096, 9), (16384, 64, 4096, 6), (16384, 64, 4096, 7),
+                         (16384, 128, 4096, 3), (16384, 128, 4096, 1), (32768, 128, 4096, 9)]:
+        _lib.check(lib.capgen_debug_gemm_variant(v))
+        print(f"v{v}", end=" ")
+        run(M, N, K, 0, 0, 0)
+elif __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "one":
+    M, N, K, ta, tb, f32, v = map(int, sys.argv[2:9])
+    _lib.check(lib.capgen_debug_gemm_variant(v))
+    run(M, N, K, ta, tb, f32)
+elif __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "sweep":
+    sweep()
+elif __name__ == "__main__":
+    shapes = [(2304, 2048, 512, 0, 0, 0), (2304, 2048, 2048, 0, 0, 0), (2304, 2048, 8192, 0, 0, 0),
+              (4096, 4096, 4096, 0, 0, 0), (2304, 6144, 512, 0, 0, 0), (1216, 10000, 512, 0, 0, 1),
+              (1216, 512, 512, 0, 1, 0), (2304, 512, 2048, 0, 1, 0), (2048, 512, 2304, 1, 1, 1),
+              (512, 512, 2304, 1, 1, 1), (1216, 512, 10000, 0, 1, 0), (512, 2176, 2304, 1, 1, 1)]
+    for sh in shapes:
+        run(*sh)
