@@ -1,8 +1,14 @@
 // capgen — fused masked attention for short sequences (Lq, Lk <= 64), one workgroup per
-// (batch, head).  Whole Q/K/V head tiles are staged in LDS as f32 (a 36x64 tile is 9 KB),
-// scores/softmax/dropout/PV never touch HBM; the softmax of one query row is one wave64
-// (lane = key) reduced with cross-lane shuffles.  The only HBM traffic is the Q/K/V read,
-// the O write and (for backward / attention_list) the f32 probabilities.
+// (batch, head).  Whole Q/K/V head tiles are staged in LDS as f32 (a 36x64 tile is 9 KB);
+// scores, softmax, dropout and P.V never touch HBM.  The softmax of one query row is one
+// wave64 (lane = key) reduced with cross-lane shuffles.  HBM traffic: the Q/K/V reads, the O
+// write and (for backward / attention_list) the f32 probabilities.
+//
+// Products are VALU f32 FMAs over 16-B LDS reads: score tiles are 2x2 register blocks
+// (4 ds_read_b128 per 16 FMAs), P.V / dS.K / P^T.dO produce 4 consecutive head columns per
+// thread (one broadcast scalar + one ds_read_b128 per 4 FMAs).  Rows are padded to dk+4
+// floats (16-B aligned, 4-bank skew), the row count to even so 2x2 blocks need no branch.
+// Every dot product runs in natural index order, so results match a sequential f32 sum.
 //
 // Semantics (modules.py:16-27, 67-92): s = (q / temperature) . k^T; masked_fill(-inf);
 // softmax; dropout; o = p . v.  Backward recomputes the dropout mask from the counter RNG.
@@ -19,18 +25,69 @@ __device__ __forceinline__ bool key_masked(const AttnGeom& g, int b, int i, int 
   return false;
 }
 
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float dot4(float4 a, float4 b, float acc) {
+  acc = fmaf(a.x, b.x, acc);
+  acc = fmaf(a.y, b.y, acc);
+  acc = fmaf(a.z, b.z, acc);
+  return fmaf(a.w, b.w, acc);
+}
+__device__ __forceinline__ void axpy4(float s, float4 v, float4& acc) {
+  acc.x = fmaf(s, v.x, acc.x);
+  acc.y = fmaf(s, v.y, acc.y);
+  acc.z = fmaf(s, v.z, acc.z);
+  acc.w = fmaf(s, v.w, acc.w);
+}
 template <typename T>
-__device__ __forceinline__ void stage_rows(float* dst, int ldd, const T* src, int64_t ld, int rows,
-                                           int dk, float mul, int tid) {
-  // rows x dk tile, 8-element (bf16) / 4-element (f32) chunks along dk
+__device__ __forceinline__ void st4(T* p, float4 v, float mul) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<float4*>(p) = float4{v.x * mul, v.y * mul, v.z * mul, v.w * mul};
+  } else {
+    typedef __attribute__((ext_vector_type(4))) __bf16 b4;
+    *reinterpret_cast<b4*>(p) = b4{(bf16)(v.x * mul), (bf16)(v.y * mul), (bf16)(v.z * mul), (bf16)(v.w * mul)};
+  }
+}
+
+// rows x dk tile -> LDS [rows_padded][ldd] f32 (x / div), zero pad row when rows is odd
+template <typename T>
+__device__ __forceinline__ void stage_rows(float* dst, int ldd, const T* src, int64_t ld, int rows, int dk,
+                                           float div, int tid) {
   constexpr int V = 16 / sizeof(T);
   const int cpr = dk / V;
   for (int c = tid; c < rows * cpr; c += AT_THREADS) {
-    int r = c / cpr, d = (c % cpr) * V;
+    const int r = c / cpr, d = (c % cpr) * V;
     float x[V];
     load_f<T, V>(src + (int64_t)r * ld + d, x);
 #pragma unroll
-    for (int e = 0; e < V; ++e) dst[r * ldd + d + e] = mul == 1.f ? x[e] : x[e] / mul;
+    for (int e = 0; e < V; ++e) dst[r * ldd + d + e] = div == 1.f ? x[e] : x[e] / div;
+  }
+  if (rows & 1)
+    for (int d = tid; d < dk; d += AT_THREADS) dst[rows * ldd + d] = 0.f;
+}
+
+// C[i][j] = sum_d X[i][d] Y[j][d] for i < R, j < Cn (2x2 register blocks)
+__device__ __forceinline__ void gram(const float* X, const float* Y, int ldd, int R, int Cn, int dk, float* C,
+                                     int ldc, int tid) {
+  const int ti = (R + 1) >> 1, tj = (Cn + 1) >> 1;
+  for (int c = tid; c < ti * tj; c += AT_THREADS) {
+    const int i0 = (c / tj) * 2, j0 = (c % tj) * 2;
+    const float* x0 = X + i0 * ldd;
+    const float* y0 = Y + j0 * ldd;
+    float a00 = 0.f, a01 = 0.f, a10 = 0.f, a11 = 0.f;
+    for (int d = 0; d < dk; d += 4) {
+      const float4 p0 = ld4(x0 + d), p1 = ld4(x0 + ldd + d);
+      const float4 q0 = ld4(y0 + d), q1 = ld4(y0 + ldd + d);
+      a00 = dot4(p0, q0, a00);
+      a01 = dot4(p0, q1, a01);
+      a10 = dot4(p1, q0, a10);
+      a11 = dot4(p1, q1, a11);
+    }
+    C[i0 * ldc + j0] = a00;
+    if (j0 + 1 < Cn) C[i0 * ldc + j0 + 1] = a01;
+    if (i0 + 1 < R) {
+      C[(i0 + 1) * ldc + j0] = a10;
+      if (j0 + 1 < Cn) C[(i0 + 1) * ldc + j0 + 1] = a11;
+    }
   }
 }
 
@@ -39,11 +96,12 @@ __global__ void __launch_bounds__(AT_THREADS) attn_fwd_kernel(AttnGeom g, T* __r
                                                               float* __restrict__ probs) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int b = blockIdx.x / g.H, h = blockIdx.x % g.H;
-  const int Lq = g.Lq, Lk = g.Lk, dk = g.dk, ldd = dk + 1, lds_s = Lk + 1;
+  const int Lq = g.Lq, Lk = g.Lk, dk = g.dk, ldd = dk + 4, lds_s = Lk + 1;
+  const int Lq2 = (Lq + 1) & ~1, Lk2 = (Lk + 1) & ~1;
   float* Qs = sm;
-  float* Ks = Qs + Lq * ldd;
-  float* Vs = Ks + Lk * ldd;
-  float* S = Vs + Lk * ldd;
+  float* Ks = Qs + Lq2 * ldd;
+  float* Vs = Ks + Lk2 * ldd;
+  float* S = Vs + Lk2 * ldd;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
   const T* q = reinterpret_cast<const T*>(g.q) + (int64_t)b * g.q_bs + h * dk;
@@ -55,14 +113,7 @@ __global__ void __launch_bounds__(AT_THREADS) attn_fwd_kernel(AttnGeom g, T* __r
   stage_rows<T>(Vs, ldd, v, g.v_ld, Lk, dk, 1.f, tid);
   __syncthreads();
 
-  for (int c = tid; c < Lq * Lk; c += AT_THREADS) {
-    int i = c / Lk, j = c % Lk;
-    const float* qi = Qs + i * ldd;
-    const float* kj = Ks + j * ldd;
-    float acc = 0.f;
-    for (int d = 0; d < dk; ++d) acc = fmaf(qi[d], kj[d], acc);
-    S[i * lds_s + j] = acc;
-  }
+  gram(Qs, Ks, ldd, Lq, Lk, dk, S, lds_s, tid);
   __syncthreads();
 
   const uint64_t seed = g.drop.seed_ptr ? *g.drop.seed_ptr : 0;
@@ -84,12 +135,13 @@ __global__ void __launch_bounds__(AT_THREADS) attn_fwd_kernel(AttnGeom g, T* __r
   __syncthreads();
 
   T* ob = o + (int64_t)b * g.o_bs + h * dk;
-  for (int c = tid; c < Lq * dk; c += AT_THREADS) {
-    int i = c / dk, d = c % dk;
+  const int d4n = dk >> 2;
+  for (int c = tid; c < Lq * d4n; c += AT_THREADS) {
+    const int i = c / d4n, d = (c % d4n) * 4;
     const float* pi = S + i * lds_s;
-    float acc = 0.f;
-    for (int j = 0; j < Lk; ++j) acc = fmaf(pi[j], Vs[j * ldd + d], acc);
-    ob[(int64_t)i * g.o_ld + d] = from_f<T>(acc);
+    float4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < Lk; ++j) axpy4(pi[j], ld4(Vs + j * ldd + d), acc);
+    st4<T>(ob + (int64_t)i * g.o_ld + d, acc, 1.f);
   }
 }
 
@@ -99,12 +151,13 @@ __global__ void __launch_bounds__(AT_THREADS) attn_bwd_kernel(AttnGeom g, const 
                                                               T* __restrict__ dkp, T* __restrict__ dvp) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int b = blockIdx.x / g.H, h = blockIdx.x % g.H;
-  const int Lq = g.Lq, Lk = g.Lk, dk = g.dk, ldd = dk + 1, lds_s = Lk + 1;
+  const int Lq = g.Lq, Lk = g.Lk, dk = g.dk, ldd = dk + 4, lds_s = Lk + 1;
+  const int Lq2 = (Lq + 1) & ~1, Lk2 = (Lk + 1) & ~1;
   float* Qs = sm;                 // q / temperature
-  float* Ks = Qs + Lq * ldd;
-  float* Vs = Ks + Lk * ldd;
-  float* dO = Vs + Lk * ldd;
-  float* Ps = dO + Lq * ldd;      // p, then dropped p
+  float* Ks = Qs + Lq2 * ldd;
+  float* Vs = Ks + Lk2 * ldd;
+  float* dO = Vs + Lk2 * ldd;
+  float* Ps = dO + Lq2 * ldd;     // p, then dropped p
   float* Ds = Ps + Lq * lds_s;    // d(p_dropped), then d(score)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
@@ -118,12 +171,7 @@ __global__ void __launch_bounds__(AT_THREADS) attn_bwd_kernel(AttnGeom g, const 
   for (int c = tid; c < Lq * Lk; c += AT_THREADS) Ps[(c / Lk) * lds_s + c % Lk] = pb[c];
   __syncthreads();
 
-  for (int c = tid; c < Lq * Lk; c += AT_THREADS) {
-    int i = c / Lk, j = c % Lk;
-    float acc = 0.f;
-    for (int d = 0; d < dk; ++d) acc = fmaf(dO[i * ldd + d], Vs[j * ldd + d], acc);
-    Ds[i * lds_s + j] = acc;
-  }
+  gram(dO, Vs, ldd, Lq, Lk, dk, Ds, lds_s, tid);  // d(p_dropped) = dO . V^T
   __syncthreads();
 
   const uint64_t seed = g.drop.seed_ptr ? *g.drop.seed_ptr : 0;
@@ -143,30 +191,34 @@ __global__ void __launch_bounds__(AT_THREADS) attn_bwd_kernel(AttnGeom g, const 
     }
     const float rs = wave_sum(p * dp);
     if (j < Lk) {
-      Ds[i * lds_s + j] = p * (dp - rs);
+      Ds[i * lds_s + j] = p * (dp - rs);  // softmax backward
       Ps[i * lds_s + j] = pd;
     }
   }
   __syncthreads();
 
+  const int d4n = dk >> 2;
   T* dkb = dkp + koff;
   T* dvb = dvp + voff;
-  for (int c = tid; c < Lk * dk; c += AT_THREADS) {
-    int j = c / dk, d = c % dk;
-    float av = 0.f, ak = 0.f;
+  for (int c = tid; c < Lk * d4n; c += AT_THREADS) {
+    const int j = c / d4n, d = (c % d4n) * 4;
+    float4 av = {0.f, 0.f, 0.f, 0.f}, ak = {0.f, 0.f, 0.f, 0.f};
     for (int i = 0; i < Lq; ++i) {
-      av = fmaf(Ps[i * lds_s + j], dO[i * ldd + d], av);
-      ak = fmaf(Ds[i * lds_s + j], Qs[i * ldd + d], ak);
+      axpy4(Ps[i * lds_s + j], ld4(dO + i * ldd + d), av);
+      axpy4(Ds[i * lds_s + j], ld4(Qs + i * ldd + d), ak);
     }
-    dvb[(int64_t)j * g.v_ld + d] = from_f<T>(av);
-    dkb[(int64_t)j * g.k_ld + d] = from_f<T>(ak);
+    st4<T>(dvb + (int64_t)j * g.v_ld + d, av, 1.f);
+    st4<T>(dkb + (int64_t)j * g.k_ld + d, ak, 1.f);
   }
   T* dqb = dq + qoff;
-  for (int c = tid; c < Lq * dk; c += AT_THREADS) {
-    int i = c / dk, d = c % dk;
-    float acc = 0.f;
-    for (int j = 0; j < Lk; ++j) acc = fmaf(Ds[i * lds_s + j], Ks[j * ldd + d], acc);
-    dqb[(int64_t)i * g.q_ld + d] = from_f<T>(acc / g.temperature);
+  for (int c = tid; c < Lq * d4n; c += AT_THREADS) {
+    const int i = c / d4n, d = (c % d4n) * 4;
+    const float* di = Ds + i * lds_s;
+    float4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < Lk; ++j) axpy4(di[j], ld4(Ks + j * ldd + d), acc);
+    // (dS . K) / temperature, as the division backward of q / temperature
+    float4 r = {acc.x / g.temperature, acc.y / g.temperature, acc.z / g.temperature, acc.w / g.temperature};
+    st4<T>(dqb + (int64_t)i * g.q_ld + d, r, 1.f);
   }
 }
 
@@ -180,38 +232,59 @@ __global__ void head_mean_kernel(const float* __restrict__ probs, int B, int H, 
   out[c] = acc / (float)H;
 }
 
-static void check_geom(const AttnGeom& g, DType t) {
+static void check_geom(const AttnGeom& g) {
   require(g.Lq >= 1 && g.Lq <= 64 && g.Lk >= 1 && g.Lk <= 64, "attention: Lq/Lk must be in [1, 64]");
   require(g.dk % 8 == 0 && g.dk <= 128, "attention: head size must be a multiple of 8 and <= 128");
-  (void)t;
+}
+
+static size_t fwd_smem(const AttnGeom& g) {
+  const size_t ldd = g.dk + 4, Lq2 = (g.Lq + 1) & ~1, Lk2 = (g.Lk + 1) & ~1;
+  return sizeof(float) * (Lq2 * ldd + 2 * Lk2 * ldd + g.Lq * (g.Lk + 1));
+}
+static size_t bwd_smem(const AttnGeom& g) {
+  const size_t ldd = g.dk + 4, Lq2 = (g.Lq + 1) & ~1, Lk2 = (g.Lk + 1) & ~1;
+  return sizeof(float) * (2 * Lq2 * ldd + 2 * Lk2 * ldd + 2 * g.Lq * (g.Lk + 1));
+}
+
+template <typename K>
+static void allow_big_lds(K kernel) {
+  static bool done = false;  // per instantiation
+  if (!done) {
+    CAPGEN_HIP(hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    done = true;
+  }
 }
 
 void attention_fwd(const AttnGeom& g, void* o, float* probs, DType t, hipStream_t s) {
-  check_geom(g, t);
-  const size_t ldd = g.dk + 1;
-  const size_t smem = sizeof(float) * (g.Lq * ldd + 2 * g.Lk * ldd + g.Lq * (g.Lk + 1));
+  check_geom(g);
+  const size_t smem = fwd_smem(g);
   require(smem <= 160 * 1024, "attention_fwd: LDS budget exceeded");
   dim3 grid(g.B * g.H);
-  if (t == DType::F32)
+  if (t == DType::F32) {
+    allow_big_lds(attn_fwd_kernel<float>);
     attn_fwd_kernel<float><<<grid, AT_THREADS, smem, s>>>(g, (float*)o, probs);
-  else
+  } else {
+    allow_big_lds(attn_fwd_kernel<bf16>);
     attn_fwd_kernel<bf16><<<grid, AT_THREADS, smem, s>>>(g, (bf16*)o, probs);
+  }
   CAPGEN_HIP(hipGetLastError());
 }
 
-void attention_bwd(const AttnGeom& g, const float* probs, const void* dout, void* dq, void* dk, void* dv,
-                   DType t, hipStream_t s) {
-  check_geom(g, t);
-  const size_t ldd = g.dk + 1;
-  const size_t smem = sizeof(float) * (2 * g.Lq * ldd + 2 * g.Lk * ldd + 2 * g.Lq * (g.Lk + 1));
+void attention_bwd(const AttnGeom& g, const float* probs, const void* dout, void* dq, void* dk, void* dv, DType t,
+                   hipStream_t s) {
+  check_geom(g);
+  const size_t smem = bwd_smem(g);
   require(smem <= 160 * 1024, "attention_bwd: LDS budget exceeded (head size too large)");
   dim3 grid(g.B * g.H);
-  if (t == DType::F32)
-    attn_bwd_kernel<float><<<grid, AT_THREADS, smem, s>>>(g, probs, (const float*)dout, (float*)dq,
-                                                          (float*)dk, (float*)dv);
-  else
+  if (t == DType::F32) {
+    allow_big_lds(attn_bwd_kernel<float>);
+    attn_bwd_kernel<float><<<grid, AT_THREADS, smem, s>>>(g, probs, (const float*)dout, (float*)dq, (float*)dk,
+                                                          (float*)dv);
+  } else {
+    allow_big_lds(attn_bwd_kernel<bf16>);
     attn_bwd_kernel<bf16><<<grid, AT_THREADS, smem, s>>>(g, probs, (const bf16*)dout, (bf16*)dq, (bf16*)dk,
                                                          (bf16*)dv);
+  }
   CAPGEN_HIP(hipGetLastError());
 }
 

@@ -82,8 +82,14 @@ struct Acts {
   float* logits;
   void* dlogits;
   float *loss_row, *grad_scale, *loss;
-  // scratch / backward
-  void *tmp, *gOut, *gRes, *gA, *gQKV, *gATT, *gH, *gQc, *gKV, *gE;
+  // scratch / backward.  gOut/gRes carry the residual-stream gradient (critical path);
+  // every other gradient buffer is per block, so the weight-gradient GEMMs that read them can
+  // run later on the side stream without a write-after-read hazard.
+  void *tmp, *gOut, *gRes, *gKV, *gE, *gAe, *gAd;
+  struct GradBufs {
+    void *gAf, *gH, *gA1, *gATT1, *gQKV, *gA2, *gATT2, *gQc;
+  };
+  std::vector<GradBufs> genc, gdec;
 };
 
 struct GenWS {
@@ -178,8 +184,9 @@ struct capgen_engine {
   Layout L;
   int device = 0;
   DType act = DType::BF16;
-  hipStream_t es = nullptr;  // engine stream
-  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  hipStream_t es = nullptr;   // engine stream (critical path)
+  hipStream_t es2 = nullptr;  // side stream: weight-gradient GEMMs
+  hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_fork = nullptr, ev_join = nullptr;
   float *params = nullptr, *grads = nullptr, *am = nullptr, *av = nullptr;
   bf16* shadow = nullptr;
   float* pe = nullptr;  // [max_length-1, dd] f32 sinusoid table
@@ -187,6 +194,11 @@ struct capgen_engine {
   float* adam_scal = nullptr;
   uint64_t* seed = nullptr;
   float* scalars = nullptr;  // internal loss
+  // striped partial sums for the small accumulated gradients (LayerNorm gamma/beta, biases):
+  // [NSTRIPE][total - enc_lng]; folded into the gradient arena by stripe_reduce
+  static constexpr int NSTRIPE = 16;
+  float* gstripe = nullptr;
+  int64_t n_small = 0;
   bool training = true;
   bool fwd_drop = true;  // dropout state of the last forward (backward must match)
   int fB = 0, fN = 0, fT = 0;  // shape of the last forward
@@ -225,6 +237,8 @@ struct capgen_engine {
   }
   const float* P(int64_t off) const { return params + off; }
   float* G(int64_t off) const { return grads + off; }
+  float* GS(int64_t off) const { return gstripe + (off - L.enc_lng); }  // striped small-gradient slot
+  void striped(LnBwd& lb) const { lb.stripes = NSTRIPE, lb.stripe_stride = n_small; }
   size_t es_() const { return dsize(act); }
   void* at(void* base, int64_t elems) const { return (char*)base + elems * es_(); }
 
@@ -253,6 +267,7 @@ struct capgen_engine {
                  int beta, const void* relu_aux, const float* alpha_ptr, hipStream_t s, float* colsum = nullptr) {
     GemmArgs ga;
     ga.colsum = colsum;
+    ga.colsum_stripes = NSTRIPE, ga.colsum_stride = n_small;  // colsum always targets gstripe
     ga.M = M, ga.N = K, ga.K = N, ga.A = dY, ga.lda = ldy, ga.B = W(woff), ga.ldb = ldw, ga.C = dX, ga.ldc = ldx;
     ga.beta = beta;
     ga.aux = relu_aux;
@@ -336,13 +351,30 @@ struct capgen_engine {
     T_(a.tmp, Mx * dmax);
     T_(a.gOut, Mx * dmax);
     T_(a.gRes, Mx * dmax);
-    T_(a.gA, Mx * dmax);
-    T_(a.gQKV, Mx * 3 * dmax);
-    T_(a.gATT, Mx * dmax);
-    T_(a.gH, Mx * std::max(L_().fe, L_().fd));
-    T_(a.gQc, Md * dd);
     T_(a.gKV, Me * L_().Ld * 2 * dd);
     T_(a.gE, Md * L_().dwe);
+    T_(a.gAe, Me * d);
+    T_(a.gAd, Md * dd);
+    a.genc.resize(L_().Le);
+    for (auto& gb : a.genc) {
+      T_(gb.gAf, Me * d);
+      T_(gb.gH, Me * L_().fe);
+      T_(gb.gA1, Me * d);
+      T_(gb.gATT1, Me * d);
+      T_(gb.gQKV, Me * 3 * d);
+      gb.gA2 = gb.gATT2 = gb.gQc = nullptr;
+    }
+    a.gdec.resize(L_().Ld);
+    for (auto& gb : a.gdec) {
+      T_(gb.gAf, Md * dd);
+      T_(gb.gH, Md * L_().fd);
+      T_(gb.gA1, Md * dd);
+      T_(gb.gATT1, Md * dd);
+      T_(gb.gQKV, Md * 3 * dd);
+      T_(gb.gA2, Md * dd);
+      T_(gb.gATT2, Md * dd);
+      T_(gb.gQc, Md * dd);
+    }
   }
   const Layout& L_() const { return L; }
 
@@ -499,44 +531,85 @@ struct capgen_engine {
   }
 
   // ------------------------------------------------------------------------------------
+  // weight-gradient GEMMs run on the side stream es2, forked from the main stream right after
+  // their inputs are produced; backward() joins es2 back at the end (both in eager mode and
+  // inside the captured graph, where this becomes a parallel branch)
+  void fork(hipStream_t s) {
+    CAPGEN_HIP(hipEventRecord(ev_fork, s));
+    CAPGEN_HIP(hipStreamWaitEvent(es2, ev_fork, 0));
+  }
+  void join(hipStream_t s) {
+    CAPGEN_HIP(hipEventRecord(ev_join, es2));
+    CAPGEN_HIP(hipStreamWaitEvent(s, ev_join, 0));
+  }
+  void dw_side(const void* dY, int64_t ldy, const void* X, int64_t ldx, int64_t goff, int64_t ldg, int M, int N,
+               int K, const float* alpha_ptr, hipStream_t s) {
+    fork(s);
+    linear_dw(dY, ldy, X, ldx, goff, ldg, M, N, K, alpha_ptr, es2);
+  }
+
   // one FFN + LayerNorm block backward; g_in = grad wrt block output, writes grad wrt the
   // block input (residual) to r_out.  X = block input, H = hidden activations.
   void ffn_bwd(int M, int d, int f, const void* g_in, const void* X, const void* H, const void* v, const float* mean,
                const float* rstd, int64_t W1, int64_t b1, int64_t W2, int64_t b2, int64_t lng, int64_t lnb,
-               RowMask mask, Drop drop, void* r_out, hipStream_t s) {
+               RowMask mask, Drop drop, void* r_out, void* gA, void* gH, hipStream_t s) {
     LnBwd lb;
     lb.M = M, lb.d = d, lb.dy = g_in, lb.v = v, lb.mean = mean, lb.rstd = rstd, lb.gamma = P(lng), lb.mask = mask;
-    lb.drop = drop, lb.d_res = r_out, lb.d_a = a.gA, lb.dgamma = G(lng), lb.dbeta = G(lnb), lb.dbias = G(b2);
+    lb.drop = drop, lb.d_res = r_out, lb.d_a = gA, lb.dgamma = GS(lng), lb.dbeta = GS(lnb), lb.dbias = GS(b2);
+    striped(lb);
     layernorm_bwd(lb, act, s);
-    linear_dw(a.gA, d, H, f, W2, f, M, d, f, nullptr, s);
-    linear_dx(a.gA, d, W2, f, a.gH, f, M, d, f, 0, H, nullptr, s, G(b1));  // x relu'(H); db1 = colsum
-    linear_dw(a.gH, f, X, d, W1, d, M, f, d, nullptr, s);
-    linear_dx(a.gH, f, W1, d, r_out, d, M, f, d, 1, nullptr, nullptr, s);
+    dw_side(gA, d, H, f, W2, f, M, d, f, nullptr, s);
+    linear_dx(gA, d, W2, f, gH, f, M, d, f, 0, H, nullptr, s, GS(b1));  // x relu'(H); db1 = colsum
+    dw_side(gH, f, X, d, W1, d, M, f, d, nullptr, s);
+    linear_dx(gH, f, W1, d, r_out, d, M, f, d, 1, nullptr, nullptr, s);
   }
   // MHA output projection + LayerNorm backward: g_in = grad wrt LN output; writes grad wrt
-  // residual (query input) into r_out and grad wrt the attention output into a.gATT.
+  // residual (query input) into r_out and grad wrt the attention output into gATT.
   void mha_out_bwd(int M, int d, const void* g_in, const void* att, const void* v, const float* mean,
-                   const float* rstd, int64_t Wo, int64_t lng, int64_t lnb, Drop drop, void* r_out, hipStream_t s) {
+                   const float* rstd, int64_t Wo, int64_t lng, int64_t lnb, Drop drop, void* r_out, void* gA,
+                   void* gATT, hipStream_t s) {
     LnBwd lb;
     lb.M = M, lb.d = d, lb.dy = g_in, lb.v = v, lb.mean = mean, lb.rstd = rstd, lb.gamma = P(lng);
-    lb.drop = drop, lb.d_res = r_out, lb.d_a = a.gA, lb.dgamma = G(lng), lb.dbeta = G(lnb);
+    lb.drop = drop, lb.d_res = r_out, lb.d_a = gA, lb.dgamma = GS(lng), lb.dbeta = GS(lnb);
+    striped(lb);
     layernorm_bwd(lb, act, s);
-    linear_dw(a.gA, d, att, d, Wo, d, M, d, d, nullptr, s);
-    linear_dx(a.gA, d, Wo, d, a.gATT, d, M, d, d, 0, nullptr, nullptr, s);
+    dw_side(gA, d, att, d, Wo, d, M, d, d, nullptr, s);
+    linear_dx(gA, d, Wo, d, gATT, d, M, d, d, 0, nullptr, nullptr, s);
   }
 
-  void backward(hipStream_t s) {
+  // Adam over arena ranges; ranges are 64-element aligned so the bf16 shadow slices line up
+  void adam_range(int64_t off, int64_t n, hipStream_t s) {
+    const int64_t ns = shadow ? std::max<int64_t>(0, std::min(n, L.n_dense - off)) : 0;
+    adam_update(params + off, grads + off, am + off, av + off, (size_t)n, cfg.beta1, cfg.beta2, cfg.eps, adam_scal,
+                ns > 0 ? shadow + off : nullptr, (size_t)ns, s);
+  }
+  void adam_decoder(hipStream_t s) {
+    adam_range(L.Wel, L.n_dense - L.Wel, s);               // Wel, decoder blocks, cross K/V, classifier
+    adam_range(L.emb, (int64_t)L.V * L.dwe, s);            // word embedding
+    adam_range(L.dec_lng, L.total - L.dec_lng, s);         // decoder LN / biases, classifier bias
+  }
+  void adam_encoder(hipStream_t s) {
+    adam_range(0, L.Wel, s);                               // feature/position embedding, encoder blocks
+    adam_range(L.enc_lng, L.dec_lng - L.enc_lng, s);       // encoder LN / biases
+  }
+
+  // overlap_adam: Adam for the decoder parameters runs on the side stream as soon as their
+  // gradients are final (while the encoder backward runs), Adam for the encoder at the end
+  void backward(hipStream_t s, bool overlap_adam = false) {
     require(fB > 0, "backward: call forward first");
     const int B = fB, N = fN, Lq = fT - 1, Me = B * N, Md = B * Lq, d = L.d, dd = L.dd;
     const int He = L.He, Hd = L.Hd, dke = d / He, dkd = dd / Hd;
     const bool on = fwd_drop;
     const float p = cfg.dropout, pa = cfg.attention_dropout;
-    // accumulated-gradient region (embedding table, LN params, biases) starts from zero
-    CAPGEN_HIP(hipMemsetAsync(grads + L.n_dense, 0, (L.total - L.n_dense) * sizeof(float), s));
+    // accumulated-gradient region (embedding table) and the striped LN/bias partials start at 0
+    CAPGEN_HIP(hipMemsetAsync(grads + L.n_dense, 0, (L.enc_lng - L.n_dense) * sizeof(float), s));
+    CAPGEN_HIP(hipMemsetAsync(gstripe, 0, (size_t)NSTRIPE * n_small * sizeof(float), s));
+    if (overlap_adam) adam_prepare(step, cfg.lr, cfg.beta1, cfg.beta2, adam_scal, s);
 
     // classifier: dlogits are unscaled (softmax - onehot); grad_scale folds 1/count (+focal)
-    column_sum(a.dlogits, Md, L.V, L.V, 1.f, a.grad_scale, G(L.bc), act, s);
-    linear_dw(a.dlogits, L.V, a.D[L.Ld], dd, L.Wc, dd, Md, L.V, dd, a.grad_scale, s);
+    fork(s);
+    column_sum(a.dlogits, Md, L.V, L.V, 1.f, a.grad_scale, GS(L.bc), act, es2, NSTRIPE, n_small);
+    linear_dw(a.dlogits, L.V, a.D[L.Ld], dd, L.Wc, dd, Md, L.V, dd, a.grad_scale, es2);
     linear_dx(a.dlogits, L.V, L.Wc, dd, a.gOut, dd, Md, L.V, dd, 0, nullptr, a.grad_scale, s);
 
     RowMask dmask{};
@@ -547,10 +620,11 @@ struct capgen_engine {
     for (int l = L.Ld - 1; l >= 0; --l) {
       const auto& w = L.dec[l];
       auto& A = a.dec[l];
+      auto& gb = a.gdec[l];
       ffn_bwd(Md, dd, L.fd, gO, A.D2, A.H, A.vf, A.mf, A.rf, w.W1, w.b1, w.W2, w.b2, w.lfg, w.lfb, dmask,
-              mk_drop(p, site(1, l, 7), on), gR, s);  // gR = grad wrt D2
+              mk_drop(p, site(1, l, 7), on), gR, gb.gAf, gb.gH, s);  // gR = grad wrt D2
       mha_out_bwd(Md, dd, gR, A.attc, A.vc, A.mc, A.rc, w.Wo_c, w.lcg, w.lcb, mk_drop(p, site(1, l, 6), on), gO,
-                  s);  // gO = grad wrt D1 (residual part)
+                  gb.gA2, gb.gATT2, s);  // gO = grad wrt D1 (residual part)
       AttnGeom c;
       c.B = B, c.H = Hd, c.Lq = Lq, c.Lk = N, c.dk = dkd;
       c.q = A.qc, c.q_ld = dd, c.q_bs = (int64_t)Lq * dd;
@@ -559,12 +633,12 @@ struct capgen_engine {
       c.o_ld = dd, c.o_bs = (int64_t)Lq * dd;
       c.temperature = std::sqrt((float)dkd);
       c.drop = mk_drop(pa, site(1, l, 5), on);
-      attention_bwd(c, A.Pc, a.gATT, a.gQc, at(a.gKV, (int64_t)l * 2 * dd), at(a.gKV, (int64_t)l * 2 * dd + dd), act,
-                    s);
-      linear_dw(a.gQc, dd, A.D1, dd, w.Wq_c, dd, Md, dd, dd, nullptr, s);
-      linear_dx(a.gQc, dd, w.Wq_c, dd, gO, dd, Md, dd, dd, 1, nullptr, nullptr, s);  // gO = grad wrt D1
+      attention_bwd(c, A.Pc, gb.gATT2, gb.gQc, at(a.gKV, (int64_t)l * 2 * dd), at(a.gKV, (int64_t)l * 2 * dd + dd),
+                    act, s);
+      dw_side(gb.gQc, dd, A.D1, dd, w.Wq_c, dd, Md, dd, dd, nullptr, s);
+      linear_dx(gb.gQc, dd, w.Wq_c, dd, gO, dd, Md, dd, dd, 1, nullptr, nullptr, s);  // gO = grad wrt D1
       mha_out_bwd(Md, dd, gO, A.atts, A.vs, A.ms, A.rs, w.Wo_s, w.lsg, w.lsb, mk_drop(p, site(1, l, 4), on), gR,
-                  s);  // gR = grad wrt D_l (residual part)
+                  gb.gA1, gb.gATT1, s);  // gR = grad wrt D_l (residual part)
       AttnGeom g;
       g.B = B, g.H = Hd, g.Lq = Lq, g.Lk = Lq, g.dk = dkd;
       g.q = A.qkv, g.q_ld = 3 * dd, g.q_bs = (int64_t)Lq * 3 * dd;
@@ -573,34 +647,44 @@ struct capgen_engine {
       g.o_ld = dd, g.o_bs = (int64_t)Lq * dd;
       g.temperature = std::sqrt((float)dkd);
       g.drop = mk_drop(pa, site(1, l, 3), on);
-      attention_bwd(g, A.Ps, a.gATT, a.gQKV, at(a.gQKV, dd), at(a.gQKV, 2 * dd), act, s);
-      linear_dw(a.gQKV, 3 * dd, a.D[l], dd, w.Wqkv, dd, Md, 3 * dd, dd, nullptr, s);
-      linear_dx(a.gQKV, 3 * dd, w.Wqkv, dd, gR, dd, Md, 3 * dd, dd, 1, nullptr, nullptr, s);
+      attention_bwd(g, A.Ps, gb.gATT1, gb.gQKV, at(gb.gQKV, dd), at(gb.gQKV, 2 * dd), act, s);
+      dw_side(gb.gQKV, 3 * dd, a.D[l], dd, w.Wqkv, dd, Md, 3 * dd, dd, nullptr, s);
+      linear_dx(gb.gQKV, 3 * dd, w.Wqkv, dd, gR, dd, Md, 3 * dd, dd, 1, nullptr, nullptr, s);
       std::swap(gO, gR);  // gO = grad wrt D_l
     }
-    // decoder embedding: LN(E.Wel^T + PE) (model.py:432-436)
+    // cross K/V of all decoder blocks -> encoder output (the encoder chain starts here)
+    dw_side(a.gKV, kvld, a.X[L.Le], d, L.Wkv_all, d, Me, L.Ld * 2 * dd, d, nullptr, s);
+    void* eO = gO == a.gOut ? a.gRes : a.gOut;  // the buffer gO is not using
+    // decoder embedding: LN(E.Wel^T + PE) (model.py:432-436) -- off the critical path
     {
       LnBwd lb;
       lb.M = Md, lb.d = dd, lb.dy = gO, lb.v = a.dv0, lb.mean = a.dm0, lb.rstd = a.dr0, lb.gamma = P(L.dec_lng);
-      lb.d_a = a.gA, lb.dgamma = G(L.dec_lng), lb.dbeta = G(L.dec_lnb);
-      layernorm_bwd(lb, act, s);
-      linear_dw(a.gA, dd, a.E, L.dwe, L.Wel, L.dwe, Md, dd, L.dwe, nullptr, s);
-      linear_dx(a.gA, dd, L.Wel, L.dwe, a.gE, L.dwe, Md, dd, L.dwe, 0, nullptr, nullptr, s);
-      embedding_scatter_add(a.gE, a.ids, Md, L.dwe, cfg.pad_idx, G(L.emb), act, s);
+      lb.d_a = a.gAd, lb.dgamma = GS(L.dec_lng), lb.dbeta = GS(L.dec_lnb);
+      striped(lb);
+      fork(s);
+      layernorm_bwd(lb, act, es2);
+      linear_dw(a.gAd, dd, a.E, L.dwe, L.Wel, L.dwe, Md, dd, L.dwe, nullptr, es2);
+      linear_dx(a.gAd, dd, L.Wel, L.dwe, a.gE, L.dwe, Md, dd, L.dwe, 0, nullptr, nullptr, es2);
+      embedding_scatter_add(a.gE, a.ids, Md, L.dwe, cfg.pad_idx, G(L.emb), act, es2);
+      // every decoder-side gradient is final here (in es2 order, after the fork above)
+      stripe_reduce(GS(L.dec_lng), NSTRIPE, n_small, L.total - L.dec_lng, G(L.dec_lng), 0, es2);
+      if (overlap_adam) adam_decoder(es2);
     }
-    // cross K/V of all decoder blocks -> encoder output
-    linear_dw(a.gKV, kvld, a.X[L.Le], d, L.Wkv_all, d, Me, L.Ld * 2 * dd, d, nullptr, s);
-    gO = a.gOut;
-    gR = a.gRes;
+    // the encoder chain must not overwrite gO (read by the decoder-embedding branch on es2):
+    // it runs on the other residual buffer and on tmp (free during backward)
+    gO = eO;
+    gR = a.tmp;
     linear_dx(a.gKV, kvld, L.Wkv_all, d, gO, d, Me, L.Ld * 2 * dd, d, 0, nullptr, nullptr, s);
     RowMask emask{};
     if (cfg.encode_mask) emask.valid = a.valid;
     for (int l = L.Le - 1; l >= 0; --l) {
       const auto& w = L.enc[l];
       auto& A = a.enc[l];
+      auto& gb = a.genc[l];
       ffn_bwd(Me, d, L.fe, gO, A.Y, A.H, A.v2, A.m2, A.r2, w.W1, w.b1, w.W2, w.b2, w.ln2g, w.ln2b, emask,
-              mk_drop(p, site(0, l, 2), on), gR, s);  // gR = grad wrt Y
-      mha_out_bwd(Me, d, gR, A.att, A.v1, A.m1, A.r1, w.Wo, w.ln1g, w.ln1b, mk_drop(p, site(0, l, 1), on), gO, s);
+              mk_drop(p, site(0, l, 2), on), gR, gb.gAf, gb.gH, s);  // gR = grad wrt Y
+      mha_out_bwd(Me, d, gR, A.att, A.v1, A.m1, A.r1, w.Wo, w.ln1g, w.ln1b, mk_drop(p, site(0, l, 1), on), gO,
+                  gb.gA1, gb.gATT1, s);
       AttnGeom g;
       g.B = B, g.H = He, g.Lq = N, g.Lk = N, g.dk = dke;
       g.q = A.qkv, g.q_ld = 3 * d, g.q_bs = (int64_t)N * 3 * d;
@@ -610,17 +694,21 @@ struct capgen_engine {
       if (cfg.encode_mask) g.key_valid = a.valid, g.kv_bs = N, g.causal = 1;
       g.temperature = std::sqrt((float)dke);
       g.drop = mk_drop(pa, site(0, l, 0), on);
-      attention_bwd(g, A.P, a.gATT, a.gQKV, at(a.gQKV, d), at(a.gQKV, 2 * d), act, s);
-      linear_dw(a.gQKV, 3 * d, a.X[l], d, w.Wqkv, d, Me, 3 * d, d, nullptr, s);
-      linear_dx(a.gQKV, 3 * d, w.Wqkv, d, gO, d, Me, 3 * d, d, 1, nullptr, nullptr, s);  // gO = grad wrt X_l
+      attention_bwd(g, A.P, gb.gATT1, gb.gQKV, at(gb.gQKV, d), at(gb.gQKV, 2 * d), act, s);
+      dw_side(gb.gQKV, 3 * d, a.X[l], d, w.Wqkv, d, Me, 3 * d, d, nullptr, s);
+      linear_dx(gb.gQKV, 3 * d, w.Wqkv, d, gO, d, Me, 3 * d, d, 1, nullptr, nullptr, s);  // gO = grad wrt X_l
     }
     {
       LnBwd lb;
       lb.M = Me, lb.d = d, lb.dy = gO, lb.v = a.ev0, lb.mean = a.em0, lb.rstd = a.er0, lb.gamma = P(L.enc_lng);
-      lb.d_a = a.gA, lb.dgamma = G(L.enc_lng), lb.dbeta = G(L.enc_lnb);
+      lb.d_a = a.gAe, lb.dgamma = GS(L.enc_lng), lb.dbeta = GS(L.enc_lnb);
+      striped(lb);
       layernorm_bwd(lb, act, s);
-      linear_dw(a.gA, d, a.Aenc, L.Kp, L.enc_emb_W, L.Kp, Me, d, L.Kp, nullptr, s);
+      dw_side(a.gAe, d, a.Aenc, L.Kp, L.enc_emb_W, L.Kp, Me, d, L.Kp, nullptr, s);
     }
+    join(s);
+    stripe_reduce(GS(L.enc_lng), NSTRIPE, n_small, L.dec_lng - L.enc_lng, G(L.enc_lng), 0, s);
+    if (overlap_adam) adam_encoder(s);
   }
 
   void allreduce_grads(hipStream_t s) {
@@ -656,9 +744,13 @@ struct capgen_engine {
     Key k{f, pos, caps, loss, (int)ft, B, N, T, training};
     auto body = [&]() {
       forward(f, ft, pos, caps, B, N, T, loss, training, es);
-      backward(es);
-      allreduce_grads(es);
-      adam(es);
+      if (!comm) {
+        backward(es, /*overlap_adam=*/true);
+      } else {
+        backward(es);
+        allreduce_grads(es);
+        adam(es);
+      }
     };
     if (!graph_on) {
       body();
@@ -901,11 +993,14 @@ struct capgen_engine {
     drop_graph();
     if (comm) ncclCommDestroy(comm);
     for (void* p : {(void*)params, (void*)grads, (void*)am, (void*)av, (void*)shadow, (void*)pe, (void*)step,
-                    (void*)adam_scal, (void*)seed, (void*)scalars, ws, gws})
+                    (void*)adam_scal, (void*)seed, (void*)scalars, (void*)gstripe, ws, gws})
       if (p) (void)hipFree(p);
     if (count_host) (void)hipHostFree(count_host);
     if (ev_in) (void)hipEventDestroy(ev_in);
     if (ev_out) (void)hipEventDestroy(ev_out);
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+    if (es2) (void)hipStreamSynchronize(es2), (void)hipStreamDestroy(es2);
     if (es) (void)hipStreamDestroy(es);
   }
 };
@@ -984,6 +1079,9 @@ int capgen_create(const capgen_config* cfg, int device, capgen_t** out) {
     h->act = dt(cfg->dtype);
     const size_t n = (size_t)h->L.total;
     CAPGEN_HIP(hipStreamCreateWithFlags(&h->es, hipStreamNonBlocking));
+    CAPGEN_HIP(hipStreamCreateWithFlags(&h->es2, hipStreamNonBlocking));
+    CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+    CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming));
     CAPGEN_HIP(hipMalloc(&h->params, n * 4));
@@ -1009,6 +1107,8 @@ int capgen_create(const capgen_config* cfg, int device, capgen_t** out) {
     uint64_t sd = cfg->seed;
     CAPGEN_HIP(hipMemcpy(h->seed, &sd, 8, hipMemcpyHostToDevice));
     CAPGEN_HIP(hipMalloc(&h->scalars, 256));
+    h->n_small = h->L.total - h->L.enc_lng;
+    CAPGEN_HIP(hipMalloc(&h->gstripe, (size_t)capgen_engine::NSTRIPE * h->n_small * sizeof(float)));
     CAPGEN_HIP(hipHostMalloc(&h->count_host, 64, hipHostMallocDefault));
     *out = h.release();
   });

@@ -24,6 +24,8 @@ struct GemmArgs {
   int beta = 0;                      // 1: accumulate into C
   int relu = 0;
   float* colsum = nullptr;           // += column sums of the (post-epilogue, beta=0) output, f32 [N]
+  int colsum_stripes = 1;            // workgroup w adds into colsum + (w % stripes) * colsum_stride
+  int64_t colsum_stride = 0;
 };
 
 // ta: A stored [K][M] (else [M][K]); tb: B stored [K][N] (else [N][K]).

@@ -222,7 +222,7 @@ void gemm(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t 
   if (in == DType::F32) {
     if (out == DType::F32) launch_layout<float, float>(g, ta, tb, s);
     else launch_layout<float, bf16>(g, ta, tb, s);
-    if (g.colsum) column_sum(g.C, g.M, g.N, g.ldc, 1.f, nullptr, g.colsum, out, s);
+    if (g.colsum) column_sum(g.C, g.M, g.N, g.ldc, 1.f, nullptr, g.colsum, out, s, g.colsum_stripes, g.colsum_stride);
   } else {
     gemm_bf16(g, out, ta, tb, s);
   }

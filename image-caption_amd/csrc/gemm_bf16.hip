@@ -285,8 +285,9 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmArgs g, int
 #pragma unroll
         for (int r = 0; r < 4; ++r) cs[r] += __shfl_xor(cs[r], o, 64);
       if (fr == 0) {
+        float* cdst = g.colsum + (int64_t)(blockIdx.x % g.colsum_stripes) * g.colsum_stride + n;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) atomicAdd(g.colsum + n + r, cs[r]);
+        for (int r = 0; r < 4; ++r) atomicAdd(cdst + r, cs[r]);
       }
     }
   }
@@ -343,23 +344,35 @@ __global__ void __launch_bounds__(256) gemm_splitk_finalize(GemmArgs g, const fl
     if (c < g.N) {
       float sum = 0.f;
       for (int r = 0; r < 16; ++r) sum += red[r][threadIdx.x];
-      atomicAdd(g.colsum + c, sum);
+      atomicAdd(g.colsum + (int64_t)(blockIdx.y % g.colsum_stripes) * g.colsum_stride + c, sum);
     }
   }
 }
 
+// split-K f32 workspaces, one per stream (GEMMs on different streams may run concurrently)
 struct Workspace {
   float* p = nullptr;
   size_t bytes = 0;
 };
-Workspace g_ws[64];
+std::map<hipStream_t, Workspace> g_ws;
+std::mutex g_ws_mu;
 
-// make sure the split-K workspace holds `bytes` (never called inside a stream capture)
-void ensure_ws(int dev, size_t bytes) {
-  if (g_ws[dev].bytes >= bytes) return;
-  if (g_ws[dev].p) CAPGEN_HIP(hipFree(g_ws[dev].p));
-  CAPGEN_HIP(hipMalloc(&g_ws[dev].p, bytes));
-  g_ws[dev].bytes = bytes;
+// make sure the stream's split-K workspace holds `bytes` (never called inside a capture)
+void ensure_ws(hipStream_t s, size_t bytes) {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  Workspace& w = g_ws[s];
+  if (w.bytes >= bytes) return;
+  if (w.p) {
+    CAPGEN_HIP(hipStreamSynchronize(s));
+    CAPGEN_HIP(hipFree(w.p));
+  }
+  CAPGEN_HIP(hipMalloc(&w.p, bytes));
+  w.bytes = bytes;
+}
+Workspace get_ws(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  auto it = g_ws.find(s);
+  return it == g_ws.end() ? Workspace{} : it->second;
 }
 
 template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int ST>
@@ -371,8 +384,9 @@ static void launch_cfg(const GemmArgs& g, hipStream_t s, int splitk) {
   float* ws = nullptr;
   if (splitk > 1) {
     const size_t bytes = (size_t)g.M * g.N * sizeof(float);
-    require(g_ws[dev].bytes >= bytes, "gemm: split-K workspace too small (tune outside capture)");
-    ws = g_ws[dev].p;
+    const Workspace w = get_ws(s);
+    require(w.bytes >= bytes, "gemm: split-K workspace too small (tune outside capture)");
+    ws = w.p;
     CAPGEN_HIP(hipMemsetAsync(ws, 0, bytes, s));
   }
   gemm_bf16_kernel<TO, TA, TB, BM, BN, WM, WN, ST>
@@ -455,7 +469,7 @@ static Choice tune(const GemmArgs& g, hipStream_t s) {
   const int nk = (g.K + BK - 1) / BK;
   for (int sk : {1, 2, 4, 8}) {
     if (sk > 1 && nk < 4 * sk) break;
-    if (sk > 1) ensure_ws(dev, (size_t)g.M * g.N * sizeof(float));
+    if (sk > 1) ensure_ws(s, (size_t)g.M * g.N * sizeof(float));
     for (int v = 1; v <= NVARIANTS; ++v) {
       launch_variant<TO, TA, TB>(v, t, s, sk);  // warm-up
       CAPGEN_HIP(hipEventRecord(e0, s));
@@ -480,11 +494,7 @@ static Choice tune(const GemmArgs& g, hipStream_t s) {
 template <typename TO, bool TA, bool TB>
 static void launch_bf16_tiles(const GemmArgs& g, hipStream_t s) {
   Choice c{g_variant % 100, std::max(1, g_variant / 100)};  // forced: variant + 100 * splitk
-  if (c.splitk > 1) {
-    int dev = 0;
-    CAPGEN_HIP(hipGetDevice(&dev));
-    ensure_ws(dev, (size_t)g.M * g.N * sizeof(float));
-  }
+  if (c.splitk > 1) ensure_ws(s, (size_t)g.M * g.N * sizeof(float));
   if (c.variant == 0) {
     c.variant = heuristic_variant(g);
     if (autotune_enabled()) {
@@ -499,6 +509,13 @@ static void launch_bf16_tiles(const GemmArgs& g, hipStream_t s) {
         if (st == hipStreamCaptureStatusNone) c = g_tuned[key] = tune<TO, TA, TB>(g, s);
       }
     }
+  }
+  if (c.splitk > 1) {
+    const size_t bytes = (size_t)g.M * g.N * sizeof(float);
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    CAPGEN_HIP(hipStreamIsCapturing(s, &st));
+    if (st == hipStreamCaptureStatusNone) ensure_ws(s, bytes);
+    else if (get_ws(s).bytes < bytes) c.splitk = 1;  // no allocation inside a capture
   }
   launch_variant<TO, TA, TB>(c.variant, g, s, c.splitk);
 }

@@ -117,6 +117,7 @@ __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(LnBwd a) {
     }
   }
   if (!a.dgamma && !a.dbias) return;
+  const int64_t so = (int64_t)(blockIdx.x % a.stripes) * a.stripe_stride;
 #pragma unroll
   for (int e = 0; e < DPL; ++e) {
     red[0][wave][c0 + e] = dg[e];
@@ -133,10 +134,10 @@ __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(LnBwd a) {
       sz += red[2][w][c];
     }
     if (a.dgamma) {
-      atomicAdd(a.dgamma + c, sg);
-      atomicAdd(a.dbeta + c, sb);
+      atomicAdd(a.dgamma + so + c, sg);
+      atomicAdd(a.dbeta + so + c, sb);
     }
-    if (a.dbias) atomicAdd(a.dbias + c, sz);
+    if (a.dbias) atomicAdd(a.dbias + so + c, sz);
   }
 }
 
@@ -288,7 +289,8 @@ void embedding_scatter_add(const void* dE, const int32_t* ids, int M, int d, int
 // 8 rows per lane), rows reduced through LDS, one atomic per column per workgroup
 template <typename T>
 __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ X, int M, int N, int64_t ldx, float alpha,
-                                                     const float* alpha_ptr, float* __restrict__ db) {
+                                                     const float* alpha_ptr, float* __restrict__ db, int stripes,
+                                                     int64_t stripe_stride) {
   constexpr int V = 16 / sizeof(T);
   __shared__ float red[32][8 * V + 1];
   const int cv = threadIdx.x & 7, rl = threadIdx.x >> 3;
@@ -319,18 +321,36 @@ __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ X, in
       float sum = 0.f;
       for (int r = 0; r < 32; ++r) sum += red[r][c];
       const float a = alpha_ptr ? alpha * *alpha_ptr : alpha;
-      atomicAdd(db + nn, a * sum);
+      atomicAdd(db + (int64_t)(blockIdx.y % stripes) * stripe_stride + nn, a * sum);
     }
   }
 }
 void column_sum(const void* X, int M, int N, int64_t ldx, float alpha, const float* alpha_ptr, float* db, DType t,
-                hipStream_t s) {
+                hipStream_t s, int stripes, int64_t stripe_stride) {
   if (M <= 0 || N <= 0) return;
   const int V = t == DType::F32 ? 4 : 8;
   require(N % V == 0 && ldx % V == 0, "column_sum: N/ld must be multiples of 16 B");
   dim3 grid((N + 8 * V - 1) / (8 * V), (M + 255) / 256);
-  if (t == DType::F32) colsum_kernel<float><<<grid, 256, 0, s>>>((const float*)X, M, N, ldx, alpha, alpha_ptr, db);
-  else colsum_kernel<bf16><<<grid, 256, 0, s>>>((const bf16*)X, M, N, ldx, alpha, alpha_ptr, db);
+  if (t == DType::F32) colsum_kernel<float><<<grid, 256, 0, s>>>((const float*)X, M, N, ldx, alpha, alpha_ptr, db, stripes,
+                                                               stripe_stride);
+  else colsum_kernel<bf16><<<grid, 256, 0, s>>>((const bf16*)X, M, N, ldx, alpha, alpha_ptr, db, stripes,
+                                                              stripe_stride);
+  CAPGEN_HIP(hipGetLastError());
+}
+
+__global__ void stripe_reduce_kernel(const float* __restrict__ S, int stripes, int64_t stride, int64_t n,
+                                     float* __restrict__ dst, int accumulate) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float acc = accumulate ? dst[i] : 0.f;
+    for (int k = 0; k < stripes; ++k) acc += S[k * stride + i];
+    dst[i] = acc;
+  }
+}
+void stripe_reduce(const float* S, int stripes, int64_t stride, int64_t n, float* dst, int accumulate,
+                   hipStream_t s) {
+  if (n <= 0) return;
+  int grid = (int)std::min<int64_t>((n + 255) / 256, 1024);
+  stripe_reduce_kernel<<<grid, 256, 0, s>>>(S, stripes, stride, n, dst, accumulate);
   CAPGEN_HIP(hipGetLastError());
 }
 
