@@ -72,6 +72,17 @@ def dominant_gemm(eng, steps=50):
             "frac": round(flops / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4)}
 
 
+def _pmc_traffic():
+    """HBM bytes per train step from the committed rocprofv3 PMC passes (FETCH_SIZE x2 per the
+    gfx950 correction + WRITE_SIZE, summed over one step's kernels; tools/pmcsum.py)."""
+    path = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        d = json.load(fh)
+    return {"bytes_per_step": d["hbm_bytes_per_step"], "source": os.path.relpath(path, REPO)}
+
+
 def cpu_baseline(cfg, steps=3, warmup=1):
     """The pinned CPU oracle (fp32 eager torch, train mode = dropout on) on this host's cores:
     a bounded sample of the same workload (same B/N/T/model), time per step -> images/s."""
@@ -145,9 +156,15 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # HIP events on the stream the step graph is launched on (the engine forks its side
+    # stream off this one and joins back, so the events bracket the whole step)
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for _ in range(args.steps):
         eng.train_step_raw(f, ft, p, c, B, N, T, loss)
+    ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -157,12 +174,16 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     final_loss = loss.item()
+    step_ms_events = ev0.elapsed_time(ev1) / args.steps
 
     images = B * world * args.steps
     value = images / elapsed
     ms = elapsed / args.steps * 1e3
     gfl_img = step_flops_per_image(cfg, N, T) / 1e9
-    achieved = value * gfl_img / 1e3 / world  # TFLOP/s per GPU
+    # roofline unit = one train-step launch (one hipGraph replay): algorithmic FLOP per step
+    # (64 images x GFLOP/image) / the event-timed average step on this GPU
+    achieved = B * gfl_img / step_ms_events   # GFLOP/ms == TFLOP/s
+    traffic = _pmc_traffic()
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
@@ -171,8 +192,12 @@ def main():
                                "f=2048, V=10000, dropout 0.3/0.1, Adam lr 5e-4",
                    "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_BF16_TFLOPS, 5), "traffic": None,
-                     "scope": f"whole train step, {gfl_img:.5f} GFLOP/image algorithmic (SURVEY §8(d))"},
+                     "frac": round(achieved / PEAK_BF16_TFLOPS, 5),
+                     "traffic": traffic["bytes_per_step"] if traffic else None,
+                     "scope": f"one train step (one graph replay) = {B} images x {gfl_img:.5f} GFLOP/image "
+                              f"algorithmic (SURVEY §8(d)); step time {step_ms_events:.4f} ms from HIP events "
+                              f"on the launch stream" + (f"; traffic = HBM bytes/step from {traffic['source']}"
+                                                         if traffic else "")},
         "final_loss": round(final_loss, 5),
     }
     if rank == 0 and world == 1:
