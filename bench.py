@@ -111,7 +111,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--graph", action="store_true", help="replay the step as one hipGraph (slower on ROCm 7)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=3)
     args = ap.parse_args()
@@ -134,8 +134,7 @@ def main():
     cfg = preset("C2", dtype=args.dtype, dropout=0.3)   # config.py:61 DROPOUT; attention 0.1
     eng = Engine(cfg, dev)
     eng.load_state_dict({k: torch.from_numpy(v) for k, v in reference_init_state_dict(cfg, seed=0).items()})
-    if args.no_graph:
-        eng.set_graph(False)
+    eng.set_graph(args.graph)
     if world > 1:
         from capgen.dp import init_engine_dp
         init_engine_dp(eng, rank, world)
@@ -156,8 +155,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    # HIP events on the stream the step graph is launched on (the engine forks its side
-    # stream off this one and joins back, so the events bracket the whole step)
+    # HIP events on the stream the step is launched on (the engine forks its side streams
+    # off this one and joins them back, so the events bracket the whole step)
     stream = torch.cuda.current_stream(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
@@ -180,7 +179,7 @@ def main():
     value = images / elapsed
     ms = elapsed / args.steps * 1e3
     gfl_img = step_flops_per_image(cfg, N, T) / 1e9
-    # roofline unit = one train-step launch (one hipGraph replay): algorithmic FLOP per step
+    # roofline unit = one train step: algorithmic FLOP per step
     # (64 images x GFLOP/image) / the event-timed average step on this GPU
     achieved = B * gfl_img / step_ms_events   # GFLOP/ms == TFLOP/s
     traffic = _pmc_traffic()
@@ -194,7 +193,7 @@ def main():
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_BF16_TFLOPS, 5),
                      "traffic": traffic["bytes_per_step"] if traffic else None,
-                     "scope": f"one train step (one graph replay) = {B} images x {gfl_img:.5f} GFLOP/image "
+                     "scope": f"one train step = {B} images x {gfl_img:.5f} GFLOP/image "
                               f"algorithmic (SURVEY §8(d)); step time {step_ms_events:.4f} ms from HIP events "
                               f"on the launch stream" + (f"; traffic = HBM bytes/step from {traffic['source']}"
                                                          if traffic else "")},

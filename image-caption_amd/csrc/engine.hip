@@ -186,7 +186,9 @@ struct capgen_engine {
   DType act = DType::BF16;
   hipStream_t es = nullptr;   // engine stream (critical path)
   hipStream_t es2 = nullptr;  // side stream: weight-gradient GEMMs
+  hipStream_t ec = nullptr;   // bucket stream: per-bucket gradient all-reduce (RCCL) + Adam
   hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_b1 = nullptr, ev_b2 = nullptr, ev_cj = nullptr;
   float *params = nullptr, *grads = nullptr, *am = nullptr, *av = nullptr;
   bf16* shadow = nullptr;
   float* pe = nullptr;  // [max_length-1, dd] f32 sinusoid table
@@ -206,8 +208,11 @@ struct capgen_engine {
   void* ws = nullptr;
   GenWS g;
   void* gws = nullptr;
-  // graph
-  bool graph_on = true;
+  // graph: off by default.  Measured on MI355X / ROCm 7 (tools/launch_probe.py): a replay of
+  // the three-stream step graph costs ~3 ms of host time and runs ~0.7 ms SLOWER on the GPU
+  // than the same kernels issued eagerly on three streams (4.3 vs 5.0 ms at C2); a
+  // single-stream graph launches in 0.1 ms but loses the stream overlap (5.5 ms).
+  bool graph_on = false;
   hipGraphExec_t gexec = nullptr;
   struct Key {
     const void *f, *p, *c;
@@ -534,14 +539,14 @@ struct capgen_engine {
   // weight-gradient GEMMs run on the side stream es2, forked from the main stream right after
   // their inputs are produced; backward() joins es2 back at the end (both in eager mode and
   // inside the captured graph, where this becomes a parallel branch)
-  void fork(hipStream_t s) {
-    CAPGEN_HIP(hipEventRecord(ev_fork, s));
-    CAPGEN_HIP(hipStreamWaitEvent(es2, ev_fork, 0));
+  // `to` waits for everything issued so far on `from` (no-op when they are one stream)
+  static void dep(hipStream_t from, hipStream_t to, hipEvent_t e) {
+    if (from == to) return;
+    CAPGEN_HIP(hipEventRecord(e, from));
+    CAPGEN_HIP(hipStreamWaitEvent(to, e, 0));
   }
-  void join(hipStream_t s) {
-    CAPGEN_HIP(hipEventRecord(ev_join, es2));
-    CAPGEN_HIP(hipStreamWaitEvent(s, ev_join, 0));
-  }
+  void fork(hipStream_t s) { dep(s, es2, ev_fork); }
+  void join(hipStream_t s) { dep(es2, s, ev_join); }
   void dw_side(const void* dY, int64_t ldy, const void* X, int64_t ldx, int64_t goff, int64_t ldg, int M, int N,
                int K, const float* alpha_ptr, hipStream_t s) {
     fork(s);
@@ -583,19 +588,27 @@ struct capgen_engine {
     adam_update(params + off, grads + off, am + off, av + off, (size_t)n, cfg.beta1, cfg.beta2, cfg.eps, adam_scal,
                 ns > 0 ? shadow + off : nullptr, (size_t)ns, s);
   }
-  void adam_decoder(hipStream_t s) {
-    adam_range(L.Wel, L.n_dense - L.Wel, s);               // Wel, decoder blocks, cross K/V, classifier
-    adam_range(L.emb, (int64_t)L.V * L.dwe, s);            // word embedding
-    adam_range(L.dec_lng, L.total - L.dec_lng, s);         // decoder LN / biases, classifier bias
-  }
-  void adam_encoder(hipStream_t s) {
-    adam_range(0, L.Wel, s);                               // feature/position embedding, encoder blocks
-    adam_range(L.enc_lng, L.dec_lng - L.enc_lng, s);       // encoder LN / biases
-  }
 
-  // overlap_adam: Adam for the decoder parameters runs on the side stream as soon as their
-  // gradients are final (while the encoder backward runs), Adam for the encoder at the end
-  void backward(hipStream_t s, bool overlap_adam = false) {
+  // Step mode (train_step): the parameter update is bucketed.  A bucket is an arena range
+  // whose gradients are final and whose weights nothing later in the backward pass reads
+  // (one transformer block, the classifier, ...).  When backward reaches that point, the
+  // bucket stream ec waits for both compute streams, all-reduces the bucket's gradients
+  // over RCCL (DP) and runs Adam on it, overlapped with the rest of the backward pass.
+  // Buckets are issued in reverse layer order: 12-20 MB each at C2, one per block.
+  bool bstep = false;
+  void bucket(int64_t off, int64_t n, hipStream_t s) {
+    if (!bstep) return;
+    dep(s, ec, ev_b1);
+    dep(es2, ec, ev_b2);
+    if (comm) NCCL_CHECK(ncclAllReduce(grads + off, grads + off, (size_t)n, ncclFloat, ncclSum, comm, ec));
+    adam_range(off, n, ec);
+  }
+  int64_t enc_end(int l) const { return l + 1 < L.Le ? L.enc[l + 1].Wqkv : L.Wel; }
+  int64_t dec_end(int l) const { return l + 1 < L.Ld ? L.dec[l + 1].Wqkv : L.Wkv_all; }
+
+  // step_params: bucketed all-reduce + Adam (see bucket()); otherwise gradients only
+  void backward(hipStream_t s, bool step_params = false) {
+    bstep = step_params;
     require(fB > 0, "backward: call forward first");
     const int B = fB, N = fN, Lq = fT - 1, Me = B * N, Md = B * Lq, d = L.d, dd = L.dd;
     const int He = L.He, Hd = L.Hd, dke = d / He, dkd = dd / Hd;
@@ -604,13 +617,14 @@ struct capgen_engine {
     // accumulated-gradient region (embedding table) and the striped LN/bias partials start at 0
     CAPGEN_HIP(hipMemsetAsync(grads + L.n_dense, 0, (L.enc_lng - L.n_dense) * sizeof(float), s));
     CAPGEN_HIP(hipMemsetAsync(gstripe, 0, (size_t)NSTRIPE * n_small * sizeof(float), s));
-    if (overlap_adam) adam_prepare(step, cfg.lr, cfg.beta1, cfg.beta2, adam_scal, s);
+    if (bstep) adam_prepare(step, cfg.lr, cfg.beta1, cfg.beta2, adam_scal, s);
 
     // classifier: dlogits are unscaled (softmax - onehot); grad_scale folds 1/count (+focal)
     fork(s);
     column_sum(a.dlogits, Md, L.V, L.V, 1.f, a.grad_scale, GS(L.bc), act, es2, NSTRIPE, n_small);
     linear_dw(a.dlogits, L.V, a.D[L.Ld], dd, L.Wc, dd, Md, L.V, dd, a.grad_scale, es2);
     linear_dx(a.dlogits, L.V, L.Wc, dd, a.gOut, dd, Md, L.V, dd, 0, nullptr, a.grad_scale, s);
+    bucket(L.Wc, L.n_dense - L.Wc, s);
 
     RowMask dmask{};
     dmask.ids = a.ids, dmask.pad_idx = cfg.pad_idx;
@@ -650,6 +664,7 @@ struct capgen_engine {
       attention_bwd(g, A.Ps, gb.gATT1, gb.gQKV, at(gb.gQKV, dd), at(gb.gQKV, 2 * dd), act, s);
       dw_side(gb.gQKV, 3 * dd, a.D[l], dd, w.Wqkv, dd, Md, 3 * dd, dd, nullptr, s);
       linear_dx(gb.gQKV, 3 * dd, w.Wqkv, dd, gR, dd, Md, 3 * dd, dd, 1, nullptr, nullptr, s);
+      bucket(w.Wqkv, dec_end(l) - w.Wqkv, s);
       std::swap(gO, gR);  // gO = grad wrt D_l
     }
     // cross K/V of all decoder blocks -> encoder output (the encoder chain starts here)
@@ -668,13 +683,17 @@ struct capgen_engine {
       embedding_scatter_add(a.gE, a.ids, Md, L.dwe, cfg.pad_idx, G(L.emb), act, es2);
       // every decoder-side gradient is final here (in es2 order, after the fork above)
       stripe_reduce(GS(L.dec_lng), NSTRIPE, n_small, L.total - L.dec_lng, G(L.dec_lng), 0, es2);
-      if (overlap_adam) adam_decoder(es2);
     }
     // the encoder chain must not overwrite gO (read by the decoder-embedding branch on es2):
     // it runs on the other residual buffer and on tmp (free during backward)
     gO = eO;
     gR = a.tmp;
     linear_dx(a.gKV, kvld, L.Wkv_all, d, gO, d, Me, L.Ld * 2 * dd, d, 0, nullptr, nullptr, s);
+    // the decoder-embedding branch (es2) has been issued: every decoder-side gradient is final
+    bucket(L.Wkv_all, L.Wc - L.Wkv_all, s);               // cross K/V of all decoder blocks
+    bucket(L.Wel, L.dec[0].Wqkv - L.Wel, s);              // word-embedding projection
+    bucket(L.emb, L.enc_lng - L.emb, s);                  // word embedding table
+    bucket(L.dec_lng, L.total - L.dec_lng, s);            // decoder LN / biases, classifier bias
     RowMask emask{};
     if (cfg.encode_mask) emask.valid = a.valid;
     for (int l = L.Le - 1; l >= 0; --l) {
@@ -697,6 +716,7 @@ struct capgen_engine {
       attention_bwd(g, A.P, gb.gATT1, gb.gQKV, at(gb.gQKV, d), at(gb.gQKV, 2 * d), act, s);
       dw_side(gb.gQKV, 3 * d, a.X[l], d, w.Wqkv, d, Me, 3 * d, d, nullptr, s);
       linear_dx(gb.gQKV, 3 * d, w.Wqkv, d, gO, d, Me, 3 * d, d, 1, nullptr, nullptr, s);  // gO = grad wrt X_l
+      bucket(w.Wqkv, enc_end(l) - w.Wqkv, s);
     }
     {
       LnBwd lb;
@@ -708,7 +728,12 @@ struct capgen_engine {
     }
     join(s);
     stripe_reduce(GS(L.enc_lng), NSTRIPE, n_small, L.dec_lng - L.enc_lng, G(L.enc_lng), 0, s);
-    if (overlap_adam) adam_encoder(s);
+    if (bstep) {
+      bucket(0, L.enc[0].Wqkv, s);                        // feature/position embedding
+      bucket(L.enc_lng, L.dec_lng - L.enc_lng, s);        // encoder LN / biases
+      dep(ec, s, ev_cj);
+      bstep = false;
+    }
   }
 
   void allreduce_grads(hipStream_t s) {
@@ -744,13 +769,7 @@ struct capgen_engine {
     Key k{f, pos, caps, loss, (int)ft, B, N, T, training};
     auto body = [&]() {
       forward(f, ft, pos, caps, B, N, T, loss, training, es);
-      if (!comm) {
-        backward(es, /*overlap_adam=*/true);
-      } else {
-        backward(es);
-        allreduce_grads(es);
-        adam(es);
-      }
+      backward(es, /*step_params=*/true);  // + bucketed RCCL all-reduce (DP) and Adam
     };
     if (!graph_on) {
       body();
@@ -1000,7 +1019,10 @@ struct capgen_engine {
     if (ev_out) (void)hipEventDestroy(ev_out);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
-    if (es2) (void)hipStreamSynchronize(es2), (void)hipStreamDestroy(es2);
+    for (hipEvent_t e : {ev_b1, ev_b2, ev_cj})
+      if (e) (void)hipEventDestroy(e);
+    if (ec && ec != es && ec != es2) (void)hipStreamSynchronize(ec), (void)hipStreamDestroy(ec);
+    if (es2 && es2 != es) (void)hipStreamSynchronize(es2), (void)hipStreamDestroy(es2);
     if (es) (void)hipStreamDestroy(es);
   }
 };
@@ -1079,9 +1101,18 @@ int capgen_create(const capgen_config* cfg, int device, capgen_t** out) {
     h->act = dt(cfg->dtype);
     const size_t n = (size_t)h->L.total;
     CAPGEN_HIP(hipStreamCreateWithFlags(&h->es, hipStreamNonBlocking));
-    CAPGEN_HIP(hipStreamCreateWithFlags(&h->es2, hipStreamNonBlocking));
+    // CAPGEN_STREAMS (experiment knob): 3 = critical path + weight-grad + bucket streams
+    // (default), 2 = buckets on the weight-grad stream, 1 = everything on one stream
+    const char* ns_env = std::getenv("CAPGEN_STREAMS");
+    const int nstreams = ns_env ? std::atoi(ns_env) : 3;
+    if (nstreams >= 2) CAPGEN_HIP(hipStreamCreateWithFlags(&h->es2, hipStreamNonBlocking));
+    else h->es2 = h->es;
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+    if (nstreams >= 3) CAPGEN_HIP(hipStreamCreateWithFlags(&h->ec, hipStreamNonBlocking));
+    else h->ec = h->es2;
+    for (hipEvent_t* e : {&h->ev_b1, &h->ev_b2, &h->ev_cj})
+      CAPGEN_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming));
     CAPGEN_HIP(hipMalloc(&h->params, n * 4));

@@ -91,6 +91,7 @@ def test_train_step_graph_equals_eager_fp32():
     f, p, c = _inputs(z)
     a = _engine(cfg, seed, dropout=0.3)
     b = _engine(cfg, seed, dropout=0.3)
+    a.set_graph(True)
     b.set_graph(False)
     # the first step is bit-identical; later steps may drift in the last bits because the
     # LayerNorm-gamma/bias/embedding gradient reductions use f32 atomics (order-dependent)
@@ -105,6 +106,54 @@ def test_train_step_graph_equals_eager_fp32():
     sa, sb = a.state_dict(False), b.state_dict(False)
     for k in sa:
         torch.testing.assert_close(sa[k], sb[k], atol=5e-3, rtol=0), k
+
+
+def _params_close(a, b, atol):
+    sa, sb = a.state_dict(False), b.state_dict(False)
+    for k in sa:
+        torch.testing.assert_close(sa[k], sb[k], atol=atol, rtol=0, msg=k)
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_bucketed_train_step_equals_unfused_fp32(graph):
+    """train_step issues all-reduce + Adam per bucket on the bucket stream, overlapped with
+    backward; it must equal forward -> backward -> adam_step over the whole arena."""
+    cfg, seed, z = load_fixture("c2s")
+    f, p, c = _inputs(z)
+    a = _engine(cfg, seed)
+    b = _engine(cfg, seed)
+    for e in (a, b):
+        e.set_training(False)
+    a.set_graph(graph)
+    for _ in range(3):
+        la = a.train_step(f, p, c).clone()
+        lb = b.forward(f, p, c).clone()
+        b.backward()
+        b.adam_step()
+        torch.cuda.synchronize()
+        assert abs(la.item() - lb.item()) < 1e-5 * abs(lb.item())
+    _params_close(a, b, 1e-6)
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_dp_world1_rccl_train_step_fp32(graph):
+    """The DP path (RCCL count + per-bucket gradient all-reduce on the bucket stream, inside
+    the captured step graph) at world size 1 equals the single-process step."""
+    from capgen.engine import Engine
+    cfg, seed, z = load_fixture("c1")
+    f, p, c = _inputs(z)
+    a = _engine(cfg, seed)
+    b = _engine(cfg, seed)
+    for e in (a, b):
+        e.set_training(False)
+        e.set_graph(graph)
+    a.dp_init(Engine.dp_unique_id(), 0, 1)
+    for _ in range(3):
+        la = a.train_step(f, p, c).clone()
+        lb = b.train_step(f, p, c).clone()
+        torch.cuda.synchronize()
+        assert abs(la.item() - lb.item()) < 1e-5 * abs(lb.item())
+    _params_close(a, b, 1e-6)
 
 
 @pytest.mark.parametrize("tag", ["c1", "c1_encmask", "c2s"])
