@@ -116,6 +116,17 @@ __device__ __forceinline__ void wait_vmcnt() {
   else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// wait until at most min(younger, MAXY) K tiles' DMA (LPT instructions each) are in flight
+template <int LPT, int MAXY>
+__device__ __forceinline__ void wait_younger(int younger) {
+  if constexpr (MAXY == 0) {
+    wait_vmcnt<0>();
+  } else {
+    if (younger >= MAXY) wait_vmcnt<MAXY * LPT>();
+    else wait_younger<LPT, MAXY - 1>(younger);
+  }
+}
+
 template <typename TO>
 __device__ __forceinline__ void load4(const TO* p, float (&v)[4]) {
   if constexpr (sizeof(TO) == 4) {
@@ -141,7 +152,8 @@ __device__ __forceinline__ void store4(TO* p, const float (&v)[4]) {
 
 template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int STAGES>
 __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmArgs g, int tiles_n, int nblk,
-                                                                const void* zero, int splitk, float* ws) {
+                                                                const void* zero, int splitk, float* ws,
+                                                                int* tile_cnt) {
   constexpr int NW = WM * WN;
   typedef Op<TA, BM, NW> OA;
   typedef Op<TB, BN, NW> OB;
@@ -187,17 +199,8 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmArgs g, int
 
   for (int kt = 0; kt < nk; ++kt) {
     // tile kt landed for this wave (up to STAGES-2 younger tiles may still fly) ...
-    const int younger = min(STAGES - 2, nk - 1 - kt);
-    if constexpr (STAGES >= 4) {
-      if (younger >= 2) wait_vmcnt<2 * LPT>();
-      else if (younger == 1) wait_vmcnt<LPT>();
-      else wait_vmcnt<0>();
-    } else if constexpr (STAGES == 3) {
-      if (younger >= 1) wait_vmcnt<LPT>();
-      else wait_vmcnt<0>();
-    } else {
-      wait_vmcnt<0>();
-    }
+    static_assert((STAGES - 2) * LPT <= 63, "vmcnt range");
+    wait_younger<LPT, STAGES - 2>(nk - 1 - kt);
     __builtin_amdgcn_s_barrier();  // ... for every wave; stage (kt-1)%STAGES is free again
     if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1);
     const char* st = smem + (kt % STAGES) * SB;
@@ -218,22 +221,53 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmArgs g, int
 
   // ---- epilogue: lane holds C[m = mb + (lane&15)][n = nb + 4*(lane>>4) + 0..3] ----
   const float alpha = g.alpha_ptr ? g.alpha * *g.alpha_ptr : g.alpha;
-  if (splitk > 1) {  // partial sums -> f32 workspace; gemm_splitk_finalize applies the epilogue
-    const int fr = lane & 15, fq = lane >> 4;
+  if (splitk > 1) {
+    // Split-K combine inside the launch (the guide's counter hand-off, write-through form):
+    // every slice stores its raw partial tile to the f32 workspace with 16-B sc1 buffer stores
+    // (write-through: no L2 write-back fence), every wave drains them, one lane takes a ticket
+    // (agent atomic); the block that draws the last ticket reads the other slices with sc1
+    // loads, sums all slices in slice order (deterministic whichever block is last) and runs
+    // the normal epilogue.  Correct for any placement of a tile's slices over XCDs.
+    constexpr int NT = 64 * NW, NF = FM * FN;
+    const int tid = threadIdx.x;
+    const int64_t tile_bytes = (int64_t)splitk * NF * NT * 16;
+    char* tbase = reinterpret_cast<char*>(ws) + (int64_t)tile * tile_bytes;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(tbase, 0, (int)tile_bytes, 0x00020000);
+    typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n = n0 + wn * TN + j * 16 + fq * 4;
-      if (n >= g.N) continue;
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int m = m0 + wm * TM + i * 16 + fr;
-        if (m >= g.M) continue;
-        float* w = ws + (int64_t)m * g.N + n;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) atomicAdd(w + r, alpha * acc[i][j][r]);
-      }
+      for (int j = 0; j < FN; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rsrc,
+                                               ((split * NF + i * FN + j) * NT + tid) * 16, 0, 16 /* sc1 */);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    volatile int* flag = reinterpret_cast<volatile int*>(smem);  // staging LDS is free now
+    if (tid == 0) {
+      const int old = __hip_atomic_fetch_add(tile_cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == splitk - 1;
+      if (last) __hip_atomic_store(tile_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+      *flag = last;
     }
-    return;
+    __syncthreads();
+    if (!*flag) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 loads below the ticket
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int sl = 0; sl < splitk; ++sl) {
+          if (sl == split) {
+            sum += acc[i][j];
+          } else {
+            const u32x4 o = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ((sl * NF + i * FN + j) * NT + tid) * 16, 0,
+                                                                  16 /* sc1 */);
+            sum += __builtin_bit_cast(f32x4, o);
+          }
+        }
+        acc[i][j] = sum;
+      }
   }
   TO* __restrict__ C = reinterpret_cast<TO*>(g.C);
   const bf16* __restrict__ aux = reinterpret_cast<const bf16*>(g.aux);
@@ -293,67 +327,13 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmArgs g, int
   }
 }
 
-// split-K epilogue: C = epi(ws) over 64x64 tiles; colsum reduced per workgroup through LDS
-template <typename TO>
-__global__ void __launch_bounds__(256) gemm_splitk_finalize(GemmArgs g, const float* __restrict__ ws) {
-  __shared__ float red[16][65];
-  const int cg = threadIdx.x & 15, rl = threadIdx.x >> 4;
-  const int n = blockIdx.x * 64 + cg * 4;
-  const bf16* __restrict__ aux = reinterpret_cast<const bf16*>(g.aux);
-  TO* __restrict__ C = reinterpret_cast<TO*>(g.C);
-  float cs[4] = {0.f, 0.f, 0.f, 0.f};
-  if (n < g.N) {
-    float bn[4] = {0.f, 0.f, 0.f, 0.f};
-    if (g.bias) {
-      float4 b4 = *reinterpret_cast<const float4*>(g.bias + n);
-      bn[0] = b4.x, bn[1] = b4.y, bn[2] = b4.z, bn[3] = b4.w;
-    }
-    for (int j = 0; j < 4; ++j) {
-      const int m = blockIdx.y * 64 + rl + 16 * j;
-      if (m >= g.M) break;
-      float4 w4 = *reinterpret_cast<const float4*>(ws + (int64_t)m * g.N + n);
-      float v[4] = {w4.x + bn[0], w4.y + bn[1], w4.z + bn[2], w4.w + bn[3]};
-      if (aux) {
-        float a4[4];
-        load4<bf16>(aux + (int64_t)m * g.ldaux + n, a4);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = a4[r] > 0.f ? v[r] : 0.f;
-      }
-      if (g.relu) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-      }
-      TO* cp = C + (int64_t)m * g.ldc + n;
-      if (g.beta) {
-        float o[4];
-        load4<TO>(cp, o);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += o[r];
-      }
-      store4<TO>(cp, v);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) cs[r] += (float)(TO)v[r];
-    }
-  }
-  if (!g.colsum) return;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) red[rl][cg * 4 + r] = cs[r];
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    const int c = blockIdx.x * 64 + threadIdx.x;
-    if (c < g.N) {
-      float sum = 0.f;
-      for (int r = 0; r < 16; ++r) sum += red[r][threadIdx.x];
-      atomicAdd(g.colsum + (int64_t)(blockIdx.y % g.colsum_stripes) * g.colsum_stride + c, sum);
-    }
-  }
-}
-
 // split-K f32 workspaces, one per stream (GEMMs on different streams may run concurrently)
 struct Workspace {
   float* p = nullptr;
   size_t bytes = 0;
+  int* cnt = nullptr;  // per-tile arrival counters (zero between launches)
 };
+constexpr int kMaxTiles = 1 << 16;
 std::map<hipStream_t, Workspace> g_ws;
 std::mutex g_ws_mu;
 
@@ -361,6 +341,10 @@ std::mutex g_ws_mu;
 void ensure_ws(hipStream_t s, size_t bytes) {
   std::lock_guard<std::mutex> lk(g_ws_mu);
   Workspace& w = g_ws[s];
+  if (!w.cnt) {
+    CAPGEN_HIP(hipMalloc(&w.cnt, kMaxTiles * sizeof(int)));
+    CAPGEN_HIP(hipMemset(w.cnt, 0, kMaxTiles * sizeof(int)));
+  }
   if (w.bytes >= bytes) return;
   if (w.p) {
     CAPGEN_HIP(hipStreamSynchronize(s));
@@ -382,19 +366,21 @@ static void launch_cfg(const GemmArgs& g, hipStream_t s, int splitk) {
   int dev = 0;
   CAPGEN_HIP(hipGetDevice(&dev));
   float* ws = nullptr;
+  int* cnt = nullptr;
   if (splitk > 1) {
-    const size_t bytes = (size_t)g.M * g.N * sizeof(float);
+    const size_t bytes = (size_t)tn * tm * splitk * BM * BN * sizeof(float);
     const Workspace w = get_ws(s);
-    require(w.bytes >= bytes, "gemm: split-K workspace too small (tune outside capture)");
-    ws = w.p;
-    CAPGEN_HIP(hipMemsetAsync(ws, 0, bytes, s));
+    require(w.bytes >= bytes && w.cnt, "gemm: split-K workspace too small (tune outside capture)");
+    require(tn * tm <= kMaxTiles, "gemm: too many tiles for split-K");
+    ws = w.p, cnt = w.cnt;
   }
   gemm_bf16_kernel<TO, TA, TB, BM, BN, WM, WN, ST>
-      <<<nblk, 64 * WM * WN, 0, s>>>(g, tn, nblk, g_zero_page[dev], splitk, ws);
-  if (splitk > 1) {
-    dim3 grid((g.N + 63) / 64, (g.M + 63) / 64);
-    gemm_splitk_finalize<TO><<<grid, 256, 0, s>>>(g, ws);
-  }
+      <<<nblk, 64 * WM * WN, 0, s>>>(g, tn, nblk, g_zero_page[dev], splitk, ws, cnt);
+}
+
+// split-K workspace bound for any variant (tiles up to 256x128)
+size_t splitk_bytes(const GemmArgs& g, int splitk) {
+  return (size_t)((g.M + 255) / 256 * 256) * ((g.N + 127) / 128 * 128) * splitk * sizeof(float);
 }
 
 int g_variant = 0;  // experiment selector (capgen_debug_gemm_variant); 0 = tuned/heuristic
@@ -402,10 +388,12 @@ int g_variant = 0;  // experiment selector (capgen_debug_gemm_variant); 0 = tune
 // Tile / wave-grid / pipeline-depth variants.  Every variant accumulates the same K tiles
 // in the same order with the same MFMA sequence, so results are bit-identical across
 // variants: the choice is a pure speed decision (made per shape by the autotuner).
-constexpr int NVARIANTS = 11;
-const char* kVariantName[NVARIANTS + 1] = {"auto",        "128x128w4s3", "128x128w8s2", "128x128w4s2",
-                                           "128x64w4s2",  "64x128w4s2",  "64x64w4s2",   "64x64w4s3",
-                                           "128x64w8s2",  "256x128w16s2", "128x128w16s2", "256x64w8s2"};
+constexpr int NVARIANTS = 16;
+const char* kVariantName[NVARIANTS + 1] = {"auto",        "128x128w4s3", "128x128w8s2",  "128x128w4s2",
+                                           "128x64w4s2",  "64x128w4s2",  "64x64w4s2",    "64x64w4s3",
+                                           "128x64w8s2",  "256x128w16s2", "128x128w16s2", "256x64w8s2",
+                                           "64x64w4s4",   "64x64w4s6",   "128x64w4s4",   "64x128w4s4",
+                                           "128x128w4s4"};
 
 template <typename TO, bool TA, bool TB>
 static void launch_variant(int v, const GemmArgs& g, hipStream_t s, int sk = 1) {
@@ -421,6 +409,11 @@ static void launch_variant(int v, const GemmArgs& g, hipStream_t s, int sk = 1) 
     case 9: return launch_cfg<TO, TA, TB, 256, 128, 4, 4, 2>(g, s, sk);
     case 10: return launch_cfg<TO, TA, TB, 128, 128, 4, 4, 2>(g, s, sk);
     case 11: return launch_cfg<TO, TA, TB, 256, 64, 4, 2, 2>(g, s, sk);
+    case 12: return launch_cfg<TO, TA, TB, 64, 64, 2, 2, 4>(g, s, sk);
+    case 13: return launch_cfg<TO, TA, TB, 64, 64, 2, 2, 6>(g, s, sk);
+    case 14: return launch_cfg<TO, TA, TB, 128, 64, 2, 2, 4>(g, s, sk);
+    case 15: return launch_cfg<TO, TA, TB, 64, 128, 2, 2, 4>(g, s, sk);
+    case 16: return launch_cfg<TO, TA, TB, 128, 128, 2, 2, 4>(g, s, sk);
     default: throw Error("gemm: unknown variant");
   }
 }
@@ -467,9 +460,9 @@ static Choice tune(const GemmArgs& g, hipStream_t s) {
   Choice best{heuristic_variant(g), 1};
   float best_ms = 1e30f;
   const int nk = (g.K + BK - 1) / BK;
-  for (int sk : {1, 2, 4, 8}) {
+  for (int sk : {1, 2, 3, 4, 6, 8}) {
     if (sk > 1 && nk < 4 * sk) break;
-    if (sk > 1) ensure_ws(s, (size_t)g.M * g.N * sizeof(float));
+    if (sk > 1) ensure_ws(s, splitk_bytes(g, sk));
     for (int v = 1; v <= NVARIANTS; ++v) {
       launch_variant<TO, TA, TB>(v, t, s, sk);  // warm-up
       CAPGEN_HIP(hipEventRecord(e0, s));
@@ -494,7 +487,7 @@ static Choice tune(const GemmArgs& g, hipStream_t s) {
 template <typename TO, bool TA, bool TB>
 static void launch_bf16_tiles(const GemmArgs& g, hipStream_t s) {
   Choice c{g_variant % 100, std::max(1, g_variant / 100)};  // forced: variant + 100 * splitk
-  if (c.splitk > 1) ensure_ws(s, (size_t)g.M * g.N * sizeof(float));
+  if (c.splitk > 1) ensure_ws(s, splitk_bytes(g, c.splitk));
   if (c.variant == 0) {
     c.variant = heuristic_variant(g);
     if (autotune_enabled()) {
@@ -511,7 +504,7 @@ static void launch_bf16_tiles(const GemmArgs& g, hipStream_t s) {
     }
   }
   if (c.splitk > 1) {
-    const size_t bytes = (size_t)g.M * g.N * sizeof(float);
+    const size_t bytes = splitk_bytes(g, c.splitk);
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     CAPGEN_HIP(hipStreamIsCapturing(s, &st));
     if (st == hipStreamCaptureStatusNone) ensure_ws(s, bytes);

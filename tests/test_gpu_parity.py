@@ -250,7 +250,7 @@ def test_gemm_kernel_vs_torch(in_dt, ta, tb, M, N, K):
     assert (Cd.cpu() - ref).abs().max().item() <= tol
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 206, 403, 810])
+@pytest.mark.parametrize("variant", list(range(1, 17)) + [206, 303, 403, 612, 813, 1314])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 1)])
 def test_gemm_every_variant_and_splitk(variant, ta, tb):
     """Each tile/wave/stage variant (and split-K factor: variant + 100*splitk) computes the
@@ -270,10 +270,12 @@ def test_gemm_every_variant_and_splitk(variant, ta, tb):
     bd = bias.to(DEV)
     _lib.check(lib.capgen_debug_gemm_variant(variant))
     try:
-        _lib.check(lib.capgen_debug_gemm(M, N, K, C.c_void_p(Ad.data_ptr()), M if ta else K, ta,
-                                         C.c_void_p(Bd.data_ptr()), N if tb else K, tb, C.c_void_p(Cd.data_ptr()),
-                                         N, 1, 0, C.c_void_p(bd.data_ptr()), 1.0, 0, 0, None))
-        torch.cuda.synchronize()
+        for _ in range(3):  # repeated launches: the split-K tile tickets must re-arm themselves
+            Cd.fill_(float("nan"))
+            _lib.check(lib.capgen_debug_gemm(M, N, K, C.c_void_p(Ad.data_ptr()), M if ta else K, ta,
+                                             C.c_void_p(Bd.data_ptr()), N if tb else K, tb, C.c_void_p(Cd.data_ptr()),
+                                             N, 1, 0, C.c_void_p(bd.data_ptr()), 1.0, 0, 0, None))
+            torch.cuda.synchronize()
+            assert (Cd.cpu() - ref).abs().max().item() <= 2e-3 * np.sqrt(K)
     finally:
         _lib.check(lib.capgen_debug_gemm_variant(0))
-    assert (Cd.cpu() - ref).abs().max().item() <= 2e-3 * np.sqrt(K)

@@ -66,6 +66,38 @@ elif __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "one":
     M, N, K, ta, tb, f32, v = map(int, sys.argv[2:9])
     _lib.check(lib.capgen_debug_gemm_variant(v))
     run(M, N, K, ta, tb, f32)
+elif __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "sk":
+    # split-K study: eager launches (the split-K workspace is per stream), event timing
+    for (M, N, K, ta, tb, f32) in [(512, 512, 2304, 1, 1, 1), (2048, 512, 2304, 1, 1, 1), (2304, 512, 2048, 0, 0, 0),
+                                   (2304, 512, 2048, 0, 1, 0), (1216, 512, 10000, 0, 1, 0)]:
+        A = torch.randn((K, M) if ta else (M, K), device="cuda", dtype=torch.bfloat16)
+        B = torch.randn((K, N) if tb else (N, K), device="cuda", dtype=torch.bfloat16)
+        Cc = torch.empty(M, N, device="cuda", dtype=torch.float32 if f32 else torch.bfloat16)
+        ref = None
+        for v in (6, 12, 13, 14, 8):
+            for sk in (1, 2, 3, 4, 6):
+                _lib.check(lib.capgen_debug_gemm_variant(v + 100 * sk))
+                s = torch.cuda.current_stream()
+                call = lambda: _lib.check(lib.capgen_debug_gemm(
+                    M, N, K, C.c_void_p(A.data_ptr()), M if ta else K, ta, C.c_void_p(B.data_ptr()), N if tb else K,
+                    tb, C.c_void_p(Cc.data_ptr()), N, 1, 0 if f32 else 1, None, 1.0, 0, 0, C.c_void_p(s.cuda_stream)))
+                for _ in range(5):
+                    call()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(50):
+                    call()
+                e1.record()
+                e1.synchronize()
+                us = e0.elapsed_time(e1) * 1e3 / 50
+                out = Cc.float()
+                if ref is None:
+                    ref = out.clone()
+                err = (out - ref).abs().max().item() / ref.abs().max().item()
+                print(f"M={M} N={N} K={K} ta={ta} tb={tb} v={v} sk={sk}: {us:7.2f} us "
+                      f"{2 * M * N * K / us / 1e6:6.1f} TF/s  rel.diff {err:.1e}", flush=True)
+    _lib.check(lib.capgen_debug_gemm_variant(0))
 elif __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "sweep":
     sweep()
 elif __name__ == "__main__":
