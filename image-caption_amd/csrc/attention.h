@@ -26,6 +26,11 @@ void attention_fwd(const AttnGeom& g, void* o, float* probs, DType t, hipStream_
 // dq/dk/dv mirror the q/k/v layouts (same ld/bs).  dO uses o_ld/o_bs.
 void attention_bwd(const AttnGeom& g, const float* probs, const void* dout, void* dq, void* dk,
                    void* dv, DType t, hipStream_t s);
+// bf16 MFMA kernels (attention_mfma.hip), used by attention_fwd/bwd when attention_mfma_ok(g);
+// the backward recomputes the probabilities and never reads `probs`
+bool attention_mfma_ok(const AttnGeom& g);
+void attention_fwd_mfma(const AttnGeom& g, bf16* o, float* probs, hipStream_t s);
+void attention_bwd_mfma(const AttnGeom& g, const bf16* dout, bf16* dq, bf16* dk, bf16* dv, hipStream_t s);
 // out[b*N + j] = mean over heads of probs[b, :, row, j]   (model.py:123)
 void attention_head_mean(const float* probs, int B, int H, int Lq, int Lk, int row, float* out,
                          hipStream_t s);

@@ -257,6 +257,7 @@ static void allow_big_lds(K kernel) {
 
 void attention_fwd(const AttnGeom& g, void* o, float* probs, DType t, hipStream_t s) {
   check_geom(g);
+  if (t == DType::BF16 && attention_mfma_ok(g)) return attention_fwd_mfma(g, (bf16*)o, probs, s);
   const size_t smem = fwd_smem(g);
   require(smem <= 160 * 1024, "attention_fwd: LDS budget exceeded");
   dim3 grid(g.B * g.H);
@@ -273,6 +274,8 @@ void attention_fwd(const AttnGeom& g, void* o, float* probs, DType t, hipStream_
 void attention_bwd(const AttnGeom& g, const float* probs, const void* dout, void* dq, void* dk, void* dv, DType t,
                    hipStream_t s) {
   check_geom(g);
+  if (t == DType::BF16 && attention_mfma_ok(g))
+    return attention_bwd_mfma(g, (const bf16*)dout, (bf16*)dq, (bf16*)dk, (bf16*)dv, s);
   const size_t smem = bwd_smem(g);
   require(smem <= 160 * 1024, "attention_bwd: LDS budget exceeded (head size too large)");
   dim3 grid(g.B * g.H);

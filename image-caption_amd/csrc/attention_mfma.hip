@@ -1,0 +1,311 @@
+// capgen — bf16 MFMA attention for short sequences (Lq, Lk <= 64, head size 64), one
+// workgroup of four wave64s per (batch, head).  Used by the bf16 performance path; the f32
+// parity path keeps the exact-order VALU kernels of attention.hip.
+//
+// Every product is a v_mfma_f32_16x16x32_bf16 issued with swapped operands, so a lane ends
+// with 4 CONSECUTIVE columns of one row: lane l holds X[row = l&15][col = 16t + 4(l>>4) + r].
+// That register layout is exactly the permuted-K operand order of gemm_bf16.hip (lane group
+// g carries k = 4g..4g+3 and 16+4g..16+4g+3 of each 32-deep step), so the softmax output P and
+// the score gradient dS feed the next MFMA straight from registers, with no LDS round trip.
+// Operands whose K dimension runs down memory rows (V^T, K^T, dO^T, Q^T, Pd^T, dS^T) are read
+// from [64][64] bf16 LDS images with ds_read_b64_tr_b16, XOR-swizzled per row.
+//
+// Forward  (wave w = query rows 16w..16w+15):  S = (Q K^T)/temperature -> mask -> softmax
+//          (row max/sum: 16 values in registers + 2 cross-lane steps) -> [probs] -> dropout
+//          -> O = P V.
+// Backward (recomputes P; probs are not read):  dPd = dO V^T, dropout, dS = P (dP - rowsum),
+//          dQ = dS K / temperature (wave = query tile), then through LDS images of Pd and dS:
+//          dV = Pd^T dO, dK = dS^T Q / temperature (wave = key tile).
+// Semantics as attention.hip (modules.py:16-27): same masks, same counter-based dropout index.
+#include <cstdlib>
+
+#include "attention.h"
+
+namespace capgen {
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef short s4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4 lds_s4;
+
+constexpr int DK = 64;        // head size handled here
+constexpr int IMG = 64 * 128;  // one [64][64] bf16 image, bytes
+
+// image [row][64 cols]: 16-B chunk c of row k sits at chunk c ^ (((k >> 1) & 3) << 1)
+__device__ __forceinline__ int swz(int k, int chunk) { return chunk ^ (((k >> 1) & 3) << 1); }
+
+// fragment for "row" cb + (lane&15) (a COLUMN of the image) and K = image rows, permuted order
+__device__ __forceinline__ bf16x8 frag_t(const char* img, int cb, int ks, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int k = ks * 32 + 4 * g + q;
+  const int ch = (cb >> 3) + (p >> 1), sub = (p & 1) * 8;
+  const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + k * 128 + swz(k, ch) * 16 + sub));
+  const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + (k + 16) * 128 + swz(k + 16, ch) * 16 + sub));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+// rows [0, L) of a global [*, ld] bf16 head slice -> image (rows >= L zero), all 256 threads
+__device__ __forceinline__ void stage_image(char* img, const bf16* src, int64_t ld, int L, int tid) {
+  for (int c = tid; c < 64 * 8; c += 256) {
+    const int row = c >> 3, ch = c & 7;
+    uint4 v = {0u, 0u, 0u, 0u};
+    if (row < L) v = *reinterpret_cast<const uint4*>(src + (int64_t)row * ld + ch * 8);
+    *reinterpret_cast<uint4*>(img + row * 128 + swz(row, ch) * 16) = v;
+  }
+}
+
+// 4 consecutive columns (col % 4 == 0) of one image row from f32 registers
+__device__ __forceinline__ void put4(char* img, int row, int col, f32x4 v) {
+  const bf16x4 b = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+  *reinterpret_cast<bf16x4*>(img + row * 128 + swz(row, col >> 3) * 16 + (col & 7) * 2) = b;
+}
+
+// row fragment straight from global memory (standard K order: 8 consecutive at 8g), zero if row >= L
+__device__ __forceinline__ bf16x8 row_frag(const bf16* base, int64_t ld, int row, int L, int ks, int lane) {
+  if (row >= L) return bf16x8{};
+  return *reinterpret_cast<const bf16x8*>(base + (int64_t)row * ld + ks * 32 + (lane >> 4) * 8);
+}
+
+__device__ __forceinline__ bool masked(const AttnGeom& g, int b, int i, int j) {
+  if (j >= g.Lk) return true;
+  if (g.causal && j > g.q_pos0 + i) return true;
+  if (g.key_valid && !g.key_valid[(int64_t)(g.kv_bmod ? b % g.kv_bmod : b) * g.kv_bs + j]) return true;
+  if (g.key_ids && g.key_ids[(int64_t)b * g.kid_bs + j] == g.pad_idx) return true;
+  return false;
+}
+
+// S[q][key] for this wave's 16 query rows: s[j][r] = S[q0 + (lane&15)][16j + 4(lane>>4) + r]
+__device__ __forceinline__ void scores(const bf16* qb, int64_t q_ld, int q0, int Lq, const bf16* kb, int64_t k_ld,
+                                       int Lk, int lane, f32x4 (&s)[4]) {
+  bf16x8 qf[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) qf[ks] = row_frag(qb, q_ld, q0 + (lane & 15), Lq, ks, lane);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 kf = row_frag(kb, k_ld, 16 * j + (lane & 15), Lk, ks, lane);
+      s[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], s[j], 0, 0, 0);
+    }
+  }
+}
+
+// masked softmax of the 64-key rows held as in scores(); p = probabilities (pre-dropout)
+__device__ __forceinline__ void softmax_rows(const AttnGeom& g, int b, int q, int lane, const f32x4 (&s)[4],
+                                             f32x4 (&p)[4]) {
+  const float inv_t = 1.f / g.temperature;
+  float mx = -INFINITY;
+  f32x4 x[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int key = 16 * j + 4 * (lane >> 4) + r;
+      x[j][r] = masked(g, b, q, key) ? -INFINITY : s[j][r] * inv_t;
+      mx = fmaxf(mx, x[j][r]);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      x[j][r] = expf(x[j][r] - mx);
+      sum += x[j][r];
+    }
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) p[j][r] = x[j][r] / sum;
+}
+
+__device__ __forceinline__ bf16x8 pack8(const f32x4& lo, const f32x4& hi) {
+  return bf16x8{(bf16)lo[0], (bf16)lo[1], (bf16)lo[2], (bf16)lo[3], (bf16)hi[0], (bf16)hi[1], (bf16)hi[2], (bf16)hi[3]};
+}
+
+__device__ __forceinline__ void store4(bf16* p, f32x4 v, float mul) {
+  *reinterpret_cast<bf16x4*>(p) = bf16x4{(bf16)(v[0] * mul), (bf16)(v[1] * mul), (bf16)(v[2] * mul), (bf16)(v[3] * mul)};
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(256) attn_fwd_mfma_kernel(AttnGeom g, bf16* __restrict__ o,
+                                                            float* __restrict__ probs) {
+  __shared__ __attribute__((aligned(16))) char Vimg[IMG];
+  const int b = blockIdx.x / g.H, h = blockIdx.x % g.H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int bk = g.kv_bmod ? b % g.kv_bmod : b;
+  const bf16* qb = reinterpret_cast<const bf16*>(g.q) + (int64_t)b * g.q_bs + h * DK;
+  const bf16* kb = reinterpret_cast<const bf16*>(g.k) + (int64_t)bk * g.k_bs + h * DK;
+  const bf16* vb = reinterpret_cast<const bf16*>(g.v) + (int64_t)bk * g.v_bs + h * DK;
+  stage_image(Vimg, vb, g.v_ld, g.Lk, tid);
+
+  const int q0 = 16 * w, q = q0 + (lane & 15);
+  f32x4 s[4], p[4];
+  if (q0 < g.Lq) {
+    scores(qb, g.q_ld, q0, g.Lq, kb, g.k_ld, g.Lk, lane, s);
+    softmax_rows(g, b, q, lane, s, p);
+    const int64_t row_idx = (((int64_t)b * g.H + h) * g.Lq + q) * g.Lk;
+    if (q < g.Lq) {
+      if (probs) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = 16 * j + 4 * (lane >> 4) + r;
+            if (key < g.Lk) probs[row_idx + key] = p[j][r];
+          }
+      }
+    }
+    if (g.drop.seed_ptr) {
+      const uint64_t seed = *g.drop.seed_ptr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = 16 * j + 4 * (lane >> 4) + r;
+          const bool keep = drop_keep(seed, g.drop.site, (uint32_t)(row_idx + key), g.drop.thresh);
+          p[j][r] = keep ? p[j][r] * g.drop.scale : 0.f;
+        }
+    }
+  }
+  __syncthreads();
+  if (q0 >= g.Lq) return;
+  // O^T[d][q] = V^T[d][key] . P^T[key][q]
+  const bf16x8 pf0 = pack8(p[0], p[1]), pf1 = pack8(p[2], p[3]);
+  bf16* ob = o + (int64_t)b * g.o_bs + h * DK;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_t(Vimg, 16 * t, 0, lane), pf0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_t(Vimg, 16 * t, 1, lane), pf1, acc, 0, 0, 0);
+    if (q < g.Lq) store4(ob + (int64_t)q * g.o_ld + 16 * t + 4 * (lane >> 4), acc, 1.f);
+  }
+}
+
+__global__ void __launch_bounds__(256) attn_bwd_mfma_kernel(AttnGeom g, const bf16* __restrict__ dout,
+                                                            bf16* __restrict__ dq, bf16* __restrict__ dkp,
+                                                            bf16* __restrict__ dvp) {
+  __shared__ __attribute__((aligned(16))) char sm[5 * IMG];
+  char* Kimg = sm;             // [key][d]
+  char* dOimg = sm + IMG;      // [q][d]
+  char* Qimg = sm + 2 * IMG;   // [q][d]
+  char* Pdimg = sm + 3 * IMG;  // [q][key]  dropped probabilities
+  char* dSimg = sm + 4 * IMG;  // [q][key]  score gradient
+  const int b = blockIdx.x / g.H, h = blockIdx.x % g.H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t qoff = (int64_t)b * g.q_bs + h * DK, koff = (int64_t)b * g.k_bs + h * DK,
+                voff = (int64_t)b * g.v_bs + h * DK, ooff = (int64_t)b * g.o_bs + h * DK;
+  const bf16* qb = reinterpret_cast<const bf16*>(g.q) + qoff;
+  const bf16* kb = reinterpret_cast<const bf16*>(g.k) + koff;
+  const bf16* vb = reinterpret_cast<const bf16*>(g.v) + voff;
+  const bf16* dob = dout + ooff;
+  stage_image(Kimg, kb, g.k_ld, g.Lk, tid);
+  stage_image(dOimg, dob, g.o_ld, g.Lq, tid);
+  stage_image(Qimg, qb, g.q_ld, g.Lq, tid);
+
+  // ---- phase 1: wave w = query rows 16w..16w+15 ----
+  const int q0 = 16 * w, q = q0 + (lane & 15);
+  const float inv_t = 1.f / g.temperature;
+  f32x4 ds[4], pd[4];
+  if (q0 < g.Lq) {
+    f32x4 s[4], p[4], dp[4];
+    scores(qb, g.q_ld, q0, g.Lq, kb, g.k_ld, g.Lk, lane, s);
+    softmax_rows(g, b, q, lane, s, p);
+    scores(dob, g.o_ld, q0, g.Lq, vb, g.v_ld, g.Lk, lane, dp);  // d(p_dropped) = dO . V^T
+    const int64_t row_idx = (((int64_t)b * g.H + h) * g.Lq + q) * g.Lk;
+    const uint64_t seed = g.drop.seed_ptr ? *g.drop.seed_ptr : 0;
+    float rs = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = 16 * j + 4 * (lane >> 4) + r;
+        float d = dp[j][r], pp = p[j][r];
+        if (g.drop.seed_ptr) {
+          const bool keep = drop_keep(seed, g.drop.site, (uint32_t)(row_idx + key), g.drop.thresh);
+          d = keep ? d * g.drop.scale : 0.f;
+          pp = keep ? pp * g.drop.scale : 0.f;
+        }
+        dp[j][r] = d;
+        pd[j][r] = pp;
+        rs += p[j][r] * d;
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    const bool live = q < g.Lq;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        ds[j][r] = live ? p[j][r] * (dp[j][r] - rs) : 0.f;  // softmax backward
+        pd[j][r] = live ? pd[j][r] : 0.f;
+      }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ds[j] = pd[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    put4(Pdimg, q, 16 * j + 4 * (lane >> 4), pd[j]);
+    put4(dSimg, q, 16 * j + 4 * (lane >> 4), ds[j]);
+  }
+  __syncthreads();
+  if (q0 < g.Lq) {  // dQ^T[d][q] = K^T[d][key] . dS^T[key][q]
+    const bf16x8 f0 = pack8(ds[0], ds[1]), f1 = pack8(ds[2], ds[3]);
+    bf16* dqb = dq + qoff;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_t(Kimg, 16 * t, 0, lane), f0, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_t(Kimg, 16 * t, 1, lane), f1, acc, 0, 0, 0);
+      if (q < g.Lq) store4(dqb + (int64_t)q * g.q_ld + 16 * t + 4 * (lane >> 4), acc, inv_t);
+    }
+  }
+  // ---- phase 2: wave w = key rows 16w..16w+15; K dimension = query rows ----
+  const int k0 = 16 * w;
+  if (k0 >= g.Lk) return;
+  const int key = k0 + (lane & 15);
+  const int nks = (g.Lq + 31) / 32;
+  bf16* dvb = dvp + voff;
+  bf16* dkb = dkp + koff;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    f32x4 av = f32x4{0.f, 0.f, 0.f, 0.f}, ak = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < nks; ++ks) {
+      // dV^T[d][key] = dO^T[d][q] . Pd[q][key];  dK^T[d][key] = Q^T[d][q] . dS[q][key]
+      av = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_t(dOimg, 16 * t, ks, lane), frag_t(Pdimg, k0, ks, lane), av,
+                                                   0, 0, 0);
+      ak = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_t(Qimg, 16 * t, ks, lane), frag_t(dSimg, k0, ks, lane), ak,
+                                                   0, 0, 0);
+    }
+    if (key < g.Lk) {
+      store4(dvb + (int64_t)key * g.v_ld + 16 * t + 4 * (lane >> 4), av, 1.f);
+      store4(dkb + (int64_t)key * g.k_ld + 16 * t + 4 * (lane >> 4), ak, inv_t);
+    }
+  }
+}
+
+bool attention_mfma_ok(const AttnGeom& g) {
+  static const bool off = std::getenv("CAPGEN_ATTN_VALU") != nullptr;  // A/B experiment knob
+  return !off && g.dk == DK && g.Lq <= 64 && g.Lk <= 64 && g.q_ld % 8 == 0 && g.k_ld % 8 == 0 && g.v_ld % 8 == 0 &&
+         g.o_ld % 8 == 0 && g.q_bs % 8 == 0 && g.k_bs % 8 == 0 && g.v_bs % 8 == 0 && g.o_bs % 8 == 0;
+}
+
+void attention_fwd_mfma(const AttnGeom& g, bf16* o, float* probs, hipStream_t s) {
+  attn_fwd_mfma_kernel<<<g.B * g.H, 256, 0, s>>>(g, o, probs);
+  CAPGEN_HIP(hipGetLastError());
+}
+
+void attention_bwd_mfma(const AttnGeom& g, const bf16* dout, bf16* dq, bf16* dk, bf16* dv, hipStream_t s) {
+  attn_bwd_mfma_kernel<<<g.B * g.H, 256, 0, s>>>(g, dout, dq, dk, dv);
+  CAPGEN_HIP(hipGetLastError());
+}
+
+}  // namespace capgen

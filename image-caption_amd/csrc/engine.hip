@@ -256,6 +256,8 @@ struct capgen_engine {
     d.scale = 1.f / (1.f - p);
     return d;
   }
+  // the f32 VALU attention backward reads the saved probabilities; the bf16 MFMA one recomputes
+  bool keep_probs(const AttnGeom& g) const { return !(act == DType::BF16 && attention_mfma_ok(g)); }
   static uint32_t site(int dec, int layer, int kind) { return (uint32_t)((dec * 64 + layer) * 16 + kind); }
 
   // C[M,N] = A[M,K] . W[N,K]^T  (nn.Linear)
@@ -454,7 +456,7 @@ struct capgen_engine {
       }
       g.temperature = std::sqrt((float)dke);
       g.drop = mk_drop(pa, site(0, l, 0), drop_on);
-      attention_fwd(g, A.att, A.P, act, s);
+      attention_fwd(g, A.att, keep_probs(g) ? A.P : nullptr, act, s);
       linear(A.att, d, w.Wo, d, a.tmp, d, act, Me, d, d, nullptr, 0, s);
       LnFwd l1;
       l1.M = Me, l1.d = d, l1.a = a.tmp, l1.drop = mk_drop(p, site(0, l, 1), drop_on), l1.res = a.X[l];
@@ -497,7 +499,7 @@ struct capgen_engine {
       g.key_ids = a.ids, g.kid_bs = Lq, g.pad_idx = cfg.pad_idx, g.causal = 1;
       g.temperature = std::sqrt((float)dkd);
       g.drop = mk_drop(pa, site(1, l, 3), drop_on);
-      attention_fwd(g, A.atts, A.Ps, act, s);
+      attention_fwd(g, A.atts, keep_probs(g) ? A.Ps : nullptr, act, s);
       linear(A.atts, dd, w.Wo_s, dd, a.tmp, dd, act, Md, dd, dd, nullptr, 0, s);
       LnFwd l1;
       l1.M = Md, l1.d = dd, l1.a = a.tmp, l1.drop = mk_drop(p, site(1, l, 4), drop_on), l1.res = a.D[l];
@@ -514,7 +516,7 @@ struct capgen_engine {
       c.key_valid = a.valid, c.kv_bs = N;
       c.temperature = std::sqrt((float)dkd);
       c.drop = mk_drop(pa, site(1, l, 5), drop_on);
-      attention_fwd(c, A.attc, A.Pc, act, s);
+      attention_fwd(c, A.attc, keep_probs(c) ? A.Pc : nullptr, act, s);
       linear(A.attc, dd, w.Wo_c, dd, a.tmp, dd, act, Md, dd, dd, nullptr, 0, s);
       LnFwd l2;
       l2.M = Md, l2.d = dd, l2.a = a.tmp, l2.drop = mk_drop(p, site(1, l, 6), drop_on), l2.res = A.D1;
@@ -645,6 +647,7 @@ struct capgen_engine {
       c.k = at(a.KV, (int64_t)l * 2 * dd), c.k_ld = kvld, c.k_bs = (int64_t)N * kvld;
       c.v = at(a.KV, (int64_t)l * 2 * dd + dd), c.v_ld = kvld, c.v_bs = (int64_t)N * kvld;
       c.o_ld = dd, c.o_bs = (int64_t)Lq * dd;
+      c.key_valid = a.valid, c.kv_bs = N;  // masks as in forward (the MFMA backward recomputes P)
       c.temperature = std::sqrt((float)dkd);
       c.drop = mk_drop(pa, site(1, l, 5), on);
       attention_bwd(c, A.Pc, gb.gATT2, gb.gQc, at(a.gKV, (int64_t)l * 2 * dd), at(a.gKV, (int64_t)l * 2 * dd + dd),
@@ -659,6 +662,7 @@ struct capgen_engine {
       g.k = at(A.qkv, dd), g.k_ld = 3 * dd, g.k_bs = (int64_t)Lq * 3 * dd;
       g.v = at(A.qkv, 2 * dd), g.v_ld = 3 * dd, g.v_bs = (int64_t)Lq * 3 * dd;
       g.o_ld = dd, g.o_bs = (int64_t)Lq * dd;
+      g.key_ids = a.ids, g.kid_bs = Lq, g.pad_idx = cfg.pad_idx, g.causal = 1;  // as in forward
       g.temperature = std::sqrt((float)dkd);
       g.drop = mk_drop(pa, site(1, l, 3), on);
       attention_bwd(g, A.Ps, gb.gATT1, gb.gQKV, at(gb.gQKV, dd), at(gb.gQKV, 2 * dd), act, s);
@@ -1329,6 +1333,27 @@ int capgen_debug_gemm(int M, int N, int K, const void* A, int64_t lda, int ta, c
     ga.M = M, ga.N = N, ga.K = K, ga.A = A, ga.lda = lda, ga.B = B, ga.ldb = ldb, ga.C = Cp, ga.ldc = ldc;
     ga.bias = bias, ga.alpha = alpha, ga.beta = beta, ga.relu = relu;
     gemm(ga, dt(in_dtype), dt(out_dtype), ta != 0, tb != 0, (hipStream_t)stream);
+  });
+}
+
+int capgen_debug_attention(int dtype, int B, int H, int Lq, int Lk, int dk, const void* q, const void* k,
+                           const void* v, const unsigned char* key_valid, int causal, float temperature, void* o,
+                           float* probs, const void* dout, void* dq, void* dk_, void* dv, void* stream) {
+  return guarded([&] {
+    require(B >= 1 && H >= 1 && dk >= 1, "debug_attention: bad shape");
+    const int64_t ld = (int64_t)H * dk;
+    AttnGeom g;
+    g.B = B, g.H = H, g.Lq = Lq, g.Lk = Lk, g.dk = dk;
+    g.q = q, g.q_ld = ld, g.q_bs = Lq * ld;
+    g.k = k, g.k_ld = ld, g.k_bs = Lk * ld;
+    g.v = v, g.v_ld = ld, g.v_bs = Lk * ld;
+    g.o_ld = ld, g.o_bs = Lq * ld;
+    g.key_valid = key_valid, g.kv_bs = Lk;
+    g.causal = causal;
+    g.temperature = temperature;
+    hipStream_t s = (hipStream_t)stream;
+    attention_fwd(g, o, probs, dt(dtype), s);
+    if (dout) attention_bwd(g, probs, dout, dq, dk_, dv, dt(dtype), s);
   });
 }
 

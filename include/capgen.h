@@ -125,6 +125,14 @@ int capgen_debug_gemm(int M, int N, int K, const void* A, int64_t lda, int ta, c
 /* Experiment hook: force a GEMM tile/wave/pipeline variant (0 = production heuristic). */
 int capgen_debug_gemm_variant(int variant);
 
+/* Test hook: one masked multi-head attention forward (+ backward when dout != NULL) on packed
+ * [B, L, H*dk] tensors (row stride H*dk), dtype 0 = f32, 1 = bf16 (the kernels the engine uses
+ * for modules.py:16-27 ScaledDotProductAttention).  key_valid: optional [B][Lk] bytes (0 =
+ * masked key); causal masks keys j > i.  probs: optional [B,H,Lq,Lk] f32 output. */
+int capgen_debug_attention(int dtype, int B, int H, int Lq, int Lk, int dk, const void* q, const void* k,
+                           const void* v, const unsigned char* key_valid, int causal, float temperature, void* o,
+                           float* probs, const void* dout, void* dq, void* dk_, void* dv, void* stream);
+
 /* Data parallel (one process per GPU, RCCL over xGMI).  Rank 0 creates the 128-byte
  * unique id; the host broadcasts it (torch.distributed store) and every rank calls
  * capgen_dp_init, which also broadcasts rank 0's parameters. */

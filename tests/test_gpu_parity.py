@@ -194,6 +194,33 @@ def test_bf16_mode_loss_close(tag):
         assert abs(got - ref) <= 0.1 * ref + 1e-5, (n, got, ref)
 
 
+def test_bf16_train_mode_matches_fp32_with_dropout():
+    """bf16 path (MFMA attention, recomputed probabilities) vs the fp32 parity path, both in
+    train mode with the same counter-RNG seed: identical dropout masks, so loss and every
+    gradient agree to bf16 accuracy.  At C2 head size (64) this exercises the MFMA attention
+    forward/backward including attention dropout."""
+    cfg, seed, z = load_fixture("c2s")
+    f, p, c = _inputs(z)
+    ref = _engine(cfg, seed, dropout=0.3)
+    e = _engine(cfg, seed, dtype="bf16", dropout=0.3)
+    for x in (ref, e):
+        x.set_training(True)
+        x.set_rng_seed(1234)
+    lr = ref.forward(f, p, c).item()
+    lb = e.forward(f, p, c).item()
+    assert abs(lb - lr) < 2e-2 * abs(lr)
+    ref.backward()
+    e.backward()
+    gr, gb = ref.grads_state_dict(), e.grads_state_dict()
+    for n in gr:
+        a, b = gr[n].double(), gb[n].double()
+        rel = ((a - b).norm() / (a.norm() + 1e-12)).item()
+        # bf16 activations through 12 blocks: ~11-13 % relative L2 error on the worst tensors at
+        # this size for BOTH attention kernels (MFMA and VALU, tools/bf16_vs_fp32.py); a wrong
+        # mask or dropout index gives O(1)
+        assert rel < 0.2, (n, rel)
+
+
 def test_dropout_backward_directional_derivative_fp32():
     """Train-mode (dropout on) gradient vs a central finite difference of the same
     dropout mask (RNG reset before each forward)."""
@@ -279,3 +306,59 @@ def test_gemm_every_variant_and_splitk(variant, ta, tb):
             assert (Cd.cpu() - ref).abs().max().item() <= 2e-3 * np.sqrt(K)
     finally:
         _lib.check(lib.capgen_debug_gemm_variant(0))
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("B,H,Lq,Lk,dk,causal,mask", [
+    (3, 8, 36, 36, 64, 0, True),    # encoder self-attention, padded regions
+    (3, 8, 19, 19, 64, 1, True),    # decoder self-attention: causal + key pad
+    (3, 8, 19, 36, 64, 0, True),    # cross-attention over regions
+    (2, 8, 64, 64, 64, 1, False),   # maximum length
+    (2, 8, 33, 17, 64, 0, False),   # ragged tiles
+    (2, 4, 9, 9, 32, 1, True),      # C1 head size (VALU kernels in both dtypes)
+])
+def test_attention_kernels_vs_torch(dtype, B, H, Lq, Lk, dk, causal, mask):
+    """ScaledDotProductAttention (modules.py:16-27) forward + backward through the C ABI vs a
+    torch fp32 autograd reference: fp32 to 1e-4, bf16 (MFMA at head size 64) to bf16 accuracy."""
+    import ctypes as C
+    from capgen import _lib
+    lib = _lib.load()
+    g = torch.Generator(device="cpu").manual_seed(B * 1000 + Lq * 10 + Lk)
+    tdt = torch.float32 if dtype == "fp32" else torch.bfloat16
+    q = torch.randn(B, Lq, H * dk, generator=g).to(tdt)
+    k = torch.randn(B, Lk, H * dk, generator=g).to(tdt)
+    v = torch.randn(B, Lk, H * dk, generator=g).to(tdt)
+    do = torch.randn(B, Lq, H * dk, generator=g).to(tdt)
+    valid = torch.ones(B, Lk, dtype=torch.uint8)
+    if mask:
+        for b in range(B):
+            valid[b, max(1, Lk - 3 * b - 2):] = 0
+    temp = float(np.sqrt(dk))
+    # reference
+    qr, kr, vr = (x.float().view(B, -1, H, dk).transpose(1, 2).requires_grad_() for x in (q, k, v))
+    s = (qr / temp) @ kr.transpose(-1, -2)
+    m = valid[:, None, None, :] == 0
+    if causal:
+        m = m | torch.triu(torch.ones(Lq, Lk, dtype=torch.bool), 1)[None, None]
+    pr = torch.softmax(s.masked_fill(m, float("-inf")), -1)
+    o_ref = (pr @ vr).transpose(1, 2).reshape(B, Lq, H * dk)
+    o_ref.backward(do.float())
+    # device
+    dev = [x.to(DEV).contiguous() for x in (q, k, v, do)]
+    vd = valid.to(DEV)
+    o = torch.empty_like(dev[0])
+    probs = torch.empty(B, H, Lq, Lk, device=DEV)
+    dq, dkk, dv = (torch.empty_like(x) for x in dev[:3])
+    ptr = lambda t: C.c_void_p(t.data_ptr())
+    _lib.check(lib.capgen_debug_attention(0 if dtype == "fp32" else 1, B, H, Lq, Lk, dk, ptr(dev[0]), ptr(dev[1]),
+                                          ptr(dev[2]), ptr(vd) if mask else None, causal, temp, ptr(o), ptr(probs),
+                                          ptr(dev[3]), ptr(dq), ptr(dkk), ptr(dv), None))
+    torch.cuda.synchronize()
+    tol = 1e-4 if dtype == "fp32" else 3e-2
+    for name, got, ref in [("o", o, o_ref), ("probs", probs, pr), ("dq", dq, qr.grad.transpose(1, 2).reshape(q.shape)),
+                           ("dk", dkk, kr.grad.transpose(1, 2).reshape(k.shape)),
+                           ("dv", dv, vr.grad.transpose(1, 2).reshape(v.shape))]:
+        got = got.float().cpu()
+        ref = ref.detach().float()
+        err = (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-6)
+        assert err < tol, (name, err)
