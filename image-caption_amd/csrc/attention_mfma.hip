@@ -46,13 +46,37 @@ __device__ __forceinline__ bf16x8 frag_t(const char* img, int cb, int ks, int la
   return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
-// rows [0, L) of a global [*, ld] bf16 head slice -> image (rows >= L zero), all 256 threads
-__device__ __forceinline__ void stage_image(char* img, const bf16* src, int64_t ld, int L, int tid) {
-  for (int c = tid; c < 64 * 8; c += 256) {
-    const int row = c >> 3, ch = c & 7;
-    uint4 v = {0u, 0u, 0u, 0u};
-    if (row < L) v = *reinterpret_cast<const uint4*>(src + (int64_t)row * ld + ch * 8);
-    *reinterpret_cast<uint4*>(img + row * 128 + swz(row, ch) * 16) = v;
+// Stage NI head slices ([L_i rows][64] bf16 from global, rows >= L_i zero) into LDS images, all
+// 256 threads: every global load is issued before the first LDS write (one round trip).
+template <int NI>
+__device__ __forceinline__ void stage_images(char* const (&img)[NI], const bf16* const (&src)[NI],
+                                             const int64_t (&ld)[NI], const int (&L)[NI], int tid) {
+  uint4 v[NI][2];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = tid + 256 * u, row = c >> 3, ch = c & 7;
+      v[i][u] = row < L[i] ? *reinterpret_cast<const uint4*>(src[i] + (int64_t)row * ld[i] + ch * 8)
+                           : uint4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = tid + 256 * u, row = c >> 3, ch = c & 7;
+      *reinterpret_cast<uint4*>(img[i] + row * 128 + swz(row, ch) * 16) = v[i][u];
+    }
+}
+
+// per-key validity (key-pad masks; causal is applied per row later) -> LDS bytes
+__device__ __forceinline__ void stage_key_ok(unsigned char* kok, const AttnGeom& g, int b, int tid) {
+  if (tid < 64) {
+    const int j = tid;
+    bool ok = j < g.Lk;
+    if (ok && g.key_valid) ok = g.key_valid[(int64_t)(g.kv_bmod ? b % g.kv_bmod : b) * g.kv_bs + j] != 0;
+    if (ok && g.key_ids) ok = g.key_ids[(int64_t)b * g.kid_bs + j] != g.pad_idx;
+    kok[j] = ok;
   }
 }
 
@@ -62,40 +86,26 @@ __device__ __forceinline__ void put4(char* img, int row, int col, f32x4 v) {
   *reinterpret_cast<bf16x4*>(img + row * 128 + swz(row, col >> 3) * 16 + (col & 7) * 2) = b;
 }
 
-// row fragment straight from global memory (standard K order: 8 consecutive at 8g), zero if row >= L
-__device__ __forceinline__ bf16x8 row_frag(const bf16* base, int64_t ld, int row, int L, int ks, int lane) {
-  if (row >= L) return bf16x8{};
-  return *reinterpret_cast<const bf16x8*>(base + (int64_t)row * ld + ks * 32 + (lane >> 4) * 8);
+// row fragment of an image (standard K order: 8 consecutive columns at 32ks + 8g)
+__device__ __forceinline__ bf16x8 frag_r(const char* img, int row, int ks, int lane) {
+  return *reinterpret_cast<const bf16x8*>(img + row * 128 + swz(row, ks * 4 + (lane >> 4)) * 16);
 }
 
-__device__ __forceinline__ bool masked(const AttnGeom& g, int b, int i, int j) {
-  if (j >= g.Lk) return true;
-  if (g.causal && j > g.q_pos0 + i) return true;
-  if (g.key_valid && !g.key_valid[(int64_t)(g.kv_bmod ? b % g.kv_bmod : b) * g.kv_bs + j]) return true;
-  if (g.key_ids && g.key_ids[(int64_t)b * g.kid_bs + j] == g.pad_idx) return true;
-  return false;
-}
-
-// S[q][key] for this wave's 16 query rows: s[j][r] = S[q0 + (lane&15)][16j + 4(lane>>4) + r]
-__device__ __forceinline__ void scores(const bf16* qb, int64_t q_ld, int q0, int Lq, const bf16* kb, int64_t k_ld,
-                                       int Lk, int lane, f32x4 (&s)[4]) {
-  bf16x8 qf[2];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) qf[ks] = row_frag(qb, q_ld, q0 + (lane & 15), Lq, ks, lane);
+// X[q][key] = A_row(q) . B_row(key) for this wave's 16 rows of image A (rows q0..q0+15) against
+// the 64 rows of image B: s[j][r] = X[q0 + (lane&15)][16j + 4(lane>>4) + r]
+__device__ __forceinline__ void scores(const char* Aimg, int q0, const char* Bimg, int lane, f32x4 (&s)[4]) {
+  const bf16x8 a0 = frag_r(Aimg, q0 + (lane & 15), 0, lane), a1 = frag_r(Aimg, q0 + (lane & 15), 1, lane);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 kf = row_frag(kb, k_ld, 16 * j + (lane & 15), Lk, ks, lane);
-      s[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], s[j], 0, 0, 0);
-    }
+    s[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_r(Bimg, 16 * j + (lane & 15), 0, lane), a0, s[j], 0, 0, 0);
+    s[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_r(Bimg, 16 * j + (lane & 15), 1, lane), a1, s[j], 0, 0, 0);
   }
 }
 
 // masked softmax of the 64-key rows held as in scores(); p = probabilities (pre-dropout)
-__device__ __forceinline__ void softmax_rows(const AttnGeom& g, int b, int q, int lane, const f32x4 (&s)[4],
-                                             f32x4 (&p)[4]) {
+__device__ __forceinline__ void softmax_rows(const AttnGeom& g, const unsigned char* kok, int q, int lane,
+                                             const f32x4 (&s)[4], f32x4 (&p)[4]) {
   const float inv_t = 1.f / g.temperature;
   float mx = -INFINITY;
   f32x4 x[4];
@@ -104,7 +114,8 @@ __device__ __forceinline__ void softmax_rows(const AttnGeom& g, int b, int q, in
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int key = 16 * j + 4 * (lane >> 4) + r;
-      x[j][r] = masked(g, b, q, key) ? -INFINITY : s[j][r] * inv_t;
+      const bool m = !kok[key] || (g.causal && key > g.q_pos0 + q);
+      x[j][r] = m ? -INFINITY : s[j][r] * inv_t;
       mx = fmaxf(mx, x[j][r]);
     }
   mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
@@ -137,46 +148,51 @@ __device__ __forceinline__ void store4(bf16* p, f32x4 v, float mul) {
 
 __global__ void __launch_bounds__(256) attn_fwd_mfma_kernel(AttnGeom g, bf16* __restrict__ o,
                                                             float* __restrict__ probs) {
-  __shared__ __attribute__((aligned(16))) char Vimg[IMG];
+  __shared__ __attribute__((aligned(16))) char sm[3 * IMG + 64];
+  char* Qimg = sm;
+  char* Kimg = sm + IMG;
+  char* Vimg = sm + 2 * IMG;
+  unsigned char* kok = reinterpret_cast<unsigned char*>(sm + 3 * IMG);
   const int b = blockIdx.x / g.H, h = blockIdx.x % g.H;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int bk = g.kv_bmod ? b % g.kv_bmod : b;
-  const bf16* qb = reinterpret_cast<const bf16*>(g.q) + (int64_t)b * g.q_bs + h * DK;
-  const bf16* kb = reinterpret_cast<const bf16*>(g.k) + (int64_t)bk * g.k_bs + h * DK;
-  const bf16* vb = reinterpret_cast<const bf16*>(g.v) + (int64_t)bk * g.v_bs + h * DK;
-  stage_image(Vimg, vb, g.v_ld, g.Lk, tid);
-
-  const int q0 = 16 * w, q = q0 + (lane & 15);
-  f32x4 s[4], p[4];
-  if (q0 < g.Lq) {
-    scores(qb, g.q_ld, q0, g.Lq, kb, g.k_ld, g.Lk, lane, s);
-    softmax_rows(g, b, q, lane, s, p);
-    const int64_t row_idx = (((int64_t)b * g.H + h) * g.Lq + q) * g.Lk;
-    if (q < g.Lq) {
-      if (probs) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int key = 16 * j + 4 * (lane >> 4) + r;
-            if (key < g.Lk) probs[row_idx + key] = p[j][r];
-          }
-      }
-    }
-    if (g.drop.seed_ptr) {
-      const uint64_t seed = *g.drop.seed_ptr;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = 16 * j + 4 * (lane >> 4) + r;
-          const bool keep = drop_keep(seed, g.drop.site, (uint32_t)(row_idx + key), g.drop.thresh);
-          p[j][r] = keep ? p[j][r] * g.drop.scale : 0.f;
-        }
-    }
+  {
+    char* const img[3] = {Qimg, Kimg, Vimg};
+    const bf16* const src[3] = {reinterpret_cast<const bf16*>(g.q) + (int64_t)b * g.q_bs + h * DK,
+                                reinterpret_cast<const bf16*>(g.k) + (int64_t)bk * g.k_bs + h * DK,
+                                reinterpret_cast<const bf16*>(g.v) + (int64_t)bk * g.v_bs + h * DK};
+    const int64_t ld[3] = {g.q_ld, g.k_ld, g.v_ld};
+    const int L[3] = {g.Lq, g.Lk, g.Lk};
+    stage_images<3>(img, src, ld, L, tid);
+    stage_key_ok(kok, g, b, tid);
   }
   __syncthreads();
+  const int q0 = 16 * w, q = q0 + (lane & 15);
   if (q0 >= g.Lq) return;
+  f32x4 s[4], p[4];
+  scores(Qimg, q0, Kimg, lane, s);
+  softmax_rows(g, kok, q, lane, s, p);
+  const int64_t row_idx = (((int64_t)b * g.H + h) * g.Lq + q) * g.Lk;
+  if (probs && q < g.Lq) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = 16 * j + 4 * (lane >> 4) + r;
+        if (key < g.Lk) probs[row_idx + key] = p[j][r];
+      }
+  }
+  if (g.drop.seed_ptr) {
+    const uint64_t seed = *g.drop.seed_ptr;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = 16 * j + 4 * (lane >> 4) + r;
+        const bool keep = drop_keep(seed, g.drop.site, (uint32_t)(row_idx + key), g.drop.thresh);
+        p[j][r] = keep ? p[j][r] * g.drop.scale : 0.f;
+      }
+  }
   // O^T[d][q] = V^T[d][key] . P^T[key][q]
   const bf16x8 pf0 = pack8(p[0], p[1]), pf1 = pack8(p[2], p[3]);
   bf16* ob = o + (int64_t)b * g.o_bs + h * DK;
@@ -192,12 +208,14 @@ __global__ void __launch_bounds__(256) attn_fwd_mfma_kernel(AttnGeom g, bf16* __
 __global__ void __launch_bounds__(256) attn_bwd_mfma_kernel(AttnGeom g, const bf16* __restrict__ dout,
                                                             bf16* __restrict__ dq, bf16* __restrict__ dkp,
                                                             bf16* __restrict__ dvp) {
-  __shared__ __attribute__((aligned(16))) char sm[5 * IMG];
+  __shared__ __attribute__((aligned(16))) char sm[6 * IMG + 64];
   char* Kimg = sm;             // [key][d]
   char* dOimg = sm + IMG;      // [q][d]
   char* Qimg = sm + 2 * IMG;   // [q][d]
-  char* Pdimg = sm + 3 * IMG;  // [q][key]  dropped probabilities
-  char* dSimg = sm + 4 * IMG;  // [q][key]  score gradient
+  char* Vimg = sm + 3 * IMG;   // [key][d]
+  char* Pdimg = sm + 4 * IMG;  // [q][key]  dropped probabilities
+  char* dSimg = sm + 5 * IMG;  // [q][key]  score gradient
+  unsigned char* kok = reinterpret_cast<unsigned char*>(sm + 6 * IMG);
   const int b = blockIdx.x / g.H, h = blockIdx.x % g.H;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int64_t qoff = (int64_t)b * g.q_bs + h * DK, koff = (int64_t)b * g.k_bs + h * DK,
@@ -206,9 +224,15 @@ __global__ void __launch_bounds__(256) attn_bwd_mfma_kernel(AttnGeom g, const bf
   const bf16* kb = reinterpret_cast<const bf16*>(g.k) + koff;
   const bf16* vb = reinterpret_cast<const bf16*>(g.v) + voff;
   const bf16* dob = dout + ooff;
-  stage_image(Kimg, kb, g.k_ld, g.Lk, tid);
-  stage_image(dOimg, dob, g.o_ld, g.Lq, tid);
-  stage_image(Qimg, qb, g.q_ld, g.Lq, tid);
+  {
+    char* const img[4] = {Kimg, dOimg, Qimg, Vimg};
+    const bf16* const src[4] = {kb, dob, qb, vb};
+    const int64_t ld[4] = {g.k_ld, g.o_ld, g.q_ld, g.v_ld};
+    const int L[4] = {g.Lk, g.Lq, g.Lq, g.Lk};
+    stage_images<4>(img, src, ld, L, tid);
+    stage_key_ok(kok, g, b, tid);
+  }
+  __syncthreads();
 
   // ---- phase 1: wave w = query rows 16w..16w+15 ----
   const int q0 = 16 * w, q = q0 + (lane & 15);
@@ -216,9 +240,9 @@ __global__ void __launch_bounds__(256) attn_bwd_mfma_kernel(AttnGeom g, const bf
   f32x4 ds[4], pd[4];
   if (q0 < g.Lq) {
     f32x4 s[4], p[4], dp[4];
-    scores(qb, g.q_ld, q0, g.Lq, kb, g.k_ld, g.Lk, lane, s);
-    softmax_rows(g, b, q, lane, s, p);
-    scores(dob, g.o_ld, q0, g.Lq, vb, g.v_ld, g.Lk, lane, dp);  // d(p_dropped) = dO . V^T
+    scores(Qimg, q0, Kimg, lane, s);
+    softmax_rows(g, kok, q, lane, s, p);
+    scores(dOimg, q0, Vimg, lane, dp);  // d(p_dropped) = dO . V^T
     const int64_t row_idx = (((int64_t)b * g.H + h) * g.Lq + q) * g.Lk;
     const uint64_t seed = g.drop.seed_ptr ? *g.drop.seed_ptr : 0;
     float rs = 0.f;
