@@ -76,44 +76,60 @@ __global__ void __launch_bounds__(LN_THREADS) ln_fwd_kernel(LnFwd a) {
 template <typename T, int DPL>
 __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(LnBwd a) {
   __shared__ float red[3][LN_THREADS / 64][64 * DPL];
+  constexpr int R = 2;  // rows in flight per wave: every load of both rows is issued first
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int d = a.d, c0 = lane * DPL;
-  float dg[DPL], db[DPL], dz[DPL];
+  float dg[DPL], db[DPL], dz[DPL], gm[DPL];
 #pragma unroll
-  for (int e = 0; e < DPL; ++e) dg[e] = db[e] = dz[e] = 0.f;
+  for (int e = 0; e < DPL; ++e) dg[e] = db[e] = dz[e] = 0.f, gm[e] = a.gamma[c0 + e];
   const uint64_t seed = a.drop.seed_ptr ? *a.drop.seed_ptr : 0;
-  for (int m = blockIdx.x * (LN_THREADS / 64) + wave; m < a.M; m += gridDim.x * (LN_THREADS / 64)) {
-    const int64_t base = (int64_t)m * d + c0;
-    float dy[DPL], v[DPL];
-    load_f<T, DPL>(reinterpret_cast<const T*>(a.dy) + base, dy);
-    load_f<T, DPL>(reinterpret_cast<const T*>(a.v) + base, v);
-    const float mean = a.mean[m], rstd = a.rstd[m];
-    const float keep = row_kept(a.mask, m) ? 1.f : 0.f;
-    float g[DPL], xh[DPL], s1 = 0.f, s2 = 0.f;
+  const int stride = gridDim.x * (LN_THREADS / 64);
+  for (int m0 = blockIdx.x * (LN_THREADS / 64) + wave; m0 < a.M; m0 += R * stride) {
+    float dy[R][DPL], v[R][DPL], mean[R], rstd[R];
+    bool on[R];
 #pragma unroll
-    for (int e = 0; e < DPL; ++e) {
-      dy[e] *= keep;
-      xh[e] = (v[e] - mean) * rstd;
-      g[e] = dy[e] * a.gamma[c0 + e];
-      s1 += g[e];
-      s2 = fmaf(g[e], xh[e], s2);
-      dg[e] = fmaf(dy[e], xh[e], dg[e]);
-      db[e] += dy[e];
-    }
-    const float mg = wave_sum(s1) / (float)d, mgx = wave_sum(s2) / (float)d;
-    float dv[DPL];
-#pragma unroll
-    for (int e = 0; e < DPL; ++e) dv[e] = rstd * (g[e] - mg - xh[e] * mgx);
-    if (a.d_res) store_f<T, DPL>(reinterpret_cast<T*>(a.d_res) + base, dv);
-    if (a.d_a) {
-      if (a.drop.seed_ptr) {
-#pragma unroll
-        for (int e = 0; e < DPL; ++e)
-          dv[e] = drop_keep(seed, a.drop.site, (uint32_t)(base + e), a.drop.thresh) ? dv[e] * a.drop.scale : 0.f;
+    for (int u = 0; u < R; ++u) {
+      const int m = m0 + u * stride;
+      on[u] = m < a.M;
+      if (on[u]) {
+        const int64_t base = (int64_t)m * d + c0;
+        load_f<T, DPL>(reinterpret_cast<const T*>(a.dy) + base, dy[u]);
+        load_f<T, DPL>(reinterpret_cast<const T*>(a.v) + base, v[u]);
+        mean[u] = a.mean[m], rstd[u] = a.rstd[m];
       }
-      store_f<T, DPL>(reinterpret_cast<T*>(a.d_a) + base, dv);
+    }
 #pragma unroll
-      for (int e = 0; e < DPL; ++e) dz[e] += dv[e];
+    for (int u = 0; u < R; ++u) {
+      if (!on[u]) continue;
+      const int m = m0 + u * stride;
+      const int64_t base = (int64_t)m * d + c0;
+      const float keep = row_kept(a.mask, m) ? 1.f : 0.f;
+      float g[DPL], xh[DPL], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < DPL; ++e) {
+        const float y = dy[u][e] * keep;
+        xh[e] = (v[u][e] - mean[u]) * rstd[u];
+        g[e] = y * gm[e];
+        s1 += g[e];
+        s2 = fmaf(g[e], xh[e], s2);
+        dg[e] = fmaf(y, xh[e], dg[e]);
+        db[e] += y;
+      }
+      const float mg = wave_sum(s1) / (float)d, mgx = wave_sum(s2) / (float)d;
+      float dv[DPL];
+#pragma unroll
+      for (int e = 0; e < DPL; ++e) dv[e] = rstd[u] * (g[e] - mg - xh[e] * mgx);
+      if (a.d_res) store_f<T, DPL>(reinterpret_cast<T*>(a.d_res) + base, dv);
+      if (a.d_a) {
+        if (a.drop.seed_ptr) {
+#pragma unroll
+          for (int e = 0; e < DPL; ++e)
+            dv[e] = drop_keep(seed, a.drop.site, (uint32_t)(base + e), a.drop.thresh) ? dv[e] * a.drop.scale : 0.f;
+        }
+        store_f<T, DPL>(reinterpret_cast<T*>(a.d_a) + base, dv);
+#pragma unroll
+        for (int e = 0; e < DPL; ++e) dz[e] += dv[e];
+      }
     }
   }
   if (!a.dgamma && !a.dbias) return;
@@ -162,8 +178,8 @@ void layernorm_fwd(const LnFwd& a, DType t, hipStream_t s) {
 
 template <typename T>
 static void ln_bwd_dispatch(const LnBwd& a, hipStream_t s) {
-  // ~256 workgroups: enough waves to cover the chip, few enough dgamma/dbeta atomics
-  dim3 grid(std::min(256, (a.M + 3) / 4));
+  // two rows per wave (one loop trip at C2), <= 512 workgroups: few enough dgamma/dbeta atomics
+  dim3 grid(std::min(512, (a.M + 7) / 8));
   switch (a.d / 64) {
     case 1: ln_bwd_kernel<T, 1><<<grid, LN_THREADS, 0, s>>>(a); break;
     case 2: ln_bwd_kernel<T, 2><<<grid, LN_THREADS, 0, s>>>(a); break;
