@@ -194,6 +194,29 @@ class Engine:
                                         _stream(self.device)))
         return ids
 
+    # ---- SCST (SelfCriticNetwork) -------------------------------------------------------
+    def rl_sample(self, feats, pos, caps):
+        """Teacher-forced forward + PolicyNetwork.sample (model_RL.py:75-97): returns
+        (sample int64 [B, T-1], per-image masked mean entropy f32 [B], LM CE loss f32 [1])."""
+        f, ft, p, c = self._inputs(feats, pos, caps)
+        B, N, _ = f.shape
+        T = c.shape[1]
+        seq = torch.empty(B, T - 1, dtype=torch.int64, device=self.device)
+        ent = torch.empty(B, dtype=torch.float32, device=self.device)
+        lm = torch.empty(1, dtype=torch.float32, device=self.device)
+        _lib.check(self.lib.capgen_rl_sample(self.h, _ptr(f), ft, _ptr(p), _ptr(c), B, N, T, _ptr(seq), _ptr(ent),
+                                             _ptr(lm), _stream(self.device)))
+        return seq, ent, lm
+
+    def rl_finish(self, scores, structure_loss_weight: float, train: bool = True):
+        """ReinforcementLearningLoss (loss.py:53-76) on the last rl_sample, with per-image total
+        scores [B]; train=True also runs backward + Adam.  Returns {loss, lm, struct} [3]."""
+        sc = torch.as_tensor(scores, dtype=torch.float32).to(self.device).contiguous()
+        out = torch.empty(3, dtype=torch.float32, device=self.device)
+        _lib.check(self.lib.capgen_rl_finish(self.h, _ptr(sc), float(structure_loss_weight), _ptr(out), int(train),
+                                             _stream(self.device)))
+        return out
+
     def set_rng_seed(self, seed: int):
         _lib.check(self.lib.capgen_set_rng_seed(self.h, seed & 0xFFFFFFFFFFFFFFFF))
 

@@ -8,6 +8,7 @@ models.py:120-122).
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from .config import CapgenConfig
@@ -87,3 +88,46 @@ class TRANSFORMER(MODEL_init):
         with torch.no_grad():
             return self.model(object_features=object_features, position_features=position_features,
                               target_caption=target_caption)
+
+
+class SelfCriticNetwork(MODEL_init):
+    """Drop-in for core/models.py:137-211 (SCST, config C5): same network as TRANSFORMER
+    (PolicyNetwork, model_RL.py:10-97 = Encoder/Decoder/classifer), trained on
+    (1 - w) * CE + w * structure loss with CIDEr-D + BLEU-4 + entropy rewards (loss.py:31-220).
+
+    One step = capgen_rl_sample (GPU) -> host scoring of the greedy-from-logits samples
+    (capgen/scst.py, parity unpinned) -> capgen_rl_finish (GPU: loss, backward, Adam)."""
+
+    def __init__(self, config: CapgenConfig | None = None, word_to_idx=None, word_to_idx_path=None,
+                 device="cuda:0", state_dict=None, structure_loss_weight=0.5, cider_reward_weight=1.0,
+                 bleu_reward_weight=1.0, entropy_reward_weight=1.0, self_cider_reward_weight=1.0, df="corpus"):
+        super().__init__(word_to_idx, word_to_idx_path)
+        from .scst import RewardScorer
+        cfg = (config or CapgenConfig()).replace(num_vocab=self.num_vocab)
+        self.config = cfg
+        self.device = torch.device(device)
+        self.model = Transformer.from_config(cfg, self.device, state_dict=state_dict)
+        self.structure_loss_weight = float(structure_loss_weight)  # core/config.py:81-85
+        self.scorer = RewardScorer(self.idx_to_word, cider_reward_weight, bleu_reward_weight, entropy_reward_weight,
+                                   self_cider_reward_weight, df=df)
+
+    def _step(self, object_features, position_features, target_caption, train):
+        eng = self.model.engine
+        sample, entropy, _ = eng.rl_sample(object_features, position_features, target_caption)
+        target = torch.as_tensor(target_caption)[:, 1:].cpu().numpy()
+        reward = np.broadcast_to(self.scorer.scores(target, sample.cpu().numpy()), (sample.shape[0],))
+        total = self.scorer.total(reward, entropy.cpu().numpy())
+        out = eng.rl_finish(total, self.structure_loss_weight, train=train)
+        return out, reward
+
+    def train_step(self, batch_features, batch_positions, batch_captions):
+        """models.py:179-195: forward, sample, reward, loss.backward(), Adam step."""
+        self._step(batch_features, batch_positions, batch_captions, train=True)
+
+    def compute_loss(self, object_features, position_features, target_caption):
+        """models.py:198-211 -> {'loss', 'language_model_loss', 'structure_loss', 'reward'}
+        (config.py:65-68 keys; reward [B, 1] as in loss.py:121)."""
+        with torch.no_grad():
+            out, reward = self._step(object_features, position_features, target_caption, train=False)
+        return {"loss": out[0], "language_model_loss": out[1], "structure_loss": out[2],
+                "reward": torch.as_tensor(np.array(reward), dtype=torch.float32).view(-1, 1)}

@@ -24,6 +24,7 @@
 #include "gemm.h"
 #include "layout.h"
 #include "ops.h"
+#include "rl.h"
 
 using namespace capgen;
 
@@ -82,6 +83,9 @@ struct Acts {
   float* logits;
   void* dlogits;
   float *loss_row, *grad_scale, *loss;
+  // SCST (rl.hip): per-row sample / lse / logp[sample] / entropy, per-image entropy, scalars
+  int32_t* rl_sample;
+  float *rl_lse, *rl_logp, *rl_ent, *rl_ent_img, *rl_score, *rl_scal;
   // scratch / backward.  gOut/gRes carry the residual-stream gradient (critical path);
   // every other gradient buffer is per block, so the weight-gradient GEMMs that read them can
   // run later on the side stream without a write-after-read hazard.
@@ -354,6 +358,13 @@ struct capgen_engine {
     p.take(a.loss_row, Md);
     p.take(a.grad_scale, 4);
     p.take(a.loss, 4);
+    p.take(a.rl_sample, Md);
+    p.take(a.rl_lse, Md);
+    p.take(a.rl_logp, Md);
+    p.take(a.rl_ent, Md);
+    p.take(a.rl_ent_img, B);
+    p.take(a.rl_score, B);
+    p.take(a.rl_scal, 8);
     const int64_t dmax = std::max<int64_t>(std::max(d, dd), L_().dwe);
     T_(a.tmp, Mx * dmax);
     T_(a.gOut, Mx * dmax);
@@ -806,6 +817,43 @@ struct capgen_engine {
     }
     leave(cs);
   }
+
+  // ------------------------------------------------------------------------------------
+  // SCST (SelfCriticNetwork.train_step, models.py:179-195): rl_sample = teacher-forced forward,
+  // PolicyNetwork.sample and the per-image entropy; the host scores the samples; rl_finish =
+  // ReinforcementLearningLoss + backward + Adam.
+  void rl_sample(const void* f, DType ft, const float* pos, const int32_t* caps, int B, int N, int T,
+                 int64_t* sample_out, float* entropy_out, float* lm_out, hipStream_t cs) {
+    ensure_acts(B, N, T);
+    enter(cs);
+    const int Lq = T - 1, Md = B * Lq;
+    forward(f, ft, pos, caps, B, N, T, nullptr, training, es);
+    rl_rows(a.logits, Md, L.V, a.rl_sample, a.rl_lse, a.rl_logp, a.rl_ent, es);
+    rl_image(a.rl_sample, a.rl_ent, B, Lq, a.rl_ent_img, a.rl_scal, es);
+    if (sample_out) rl_export(a.rl_sample, Md, sample_out, es);
+    if (entropy_out) CAPGEN_HIP(hipMemcpyAsync(entropy_out, a.rl_ent_img, B * sizeof(float), hipMemcpyDeviceToDevice, es));
+    if (lm_out) CAPGEN_HIP(hipMemcpyAsync(lm_out, a.loss, sizeof(float), hipMemcpyDeviceToDevice, es));
+    rl_B = B;
+    leave(cs);
+  }
+  void rl_finish(const float* score, float w, float* out3, bool train, hipStream_t cs) {
+    require(rl_B > 0 && rl_B == fB, "rl_finish: call rl_sample first");
+    require(w >= 0.f && w <= 1.f, "rl_finish: structure_loss_weight must be in [0, 1]");
+    enter(cs);
+    const int B = fB, Lq = fT - 1;
+    CAPGEN_HIP(hipMemcpyAsync(a.rl_score, score, B * sizeof(float), hipMemcpyDeviceToDevice, es));
+    rl_numer(a.rl_sample, a.rl_logp, a.rl_score, B, Lq, a.rl_scal, es);
+    if (comm) NCCL_CHECK(ncclAllReduce(a.rl_scal, a.rl_scal, 2, ncclFloat, ncclSum, comm, es));
+    rl_loss(a.rl_scal, a.loss, w, out3 ? out3 : a.rl_scal + 2, a.grad_scale, es);
+    if (train) {
+      rl_grad(a.logits, a.tgt, a.rl_sample, a.rl_lse, a.rl_score, a.count, a.rl_scal, B, Lq, L.V, cfg.pad_idx, w,
+              a.dlogits, act, es);
+      backward(es, /*step_params=*/true);
+    }
+    rl_B = 0;
+    leave(cs);
+  }
+  int rl_B = 0;
 
   // ------------------------------------------------------------------------------------
   // decoding (model.py:101-200), KV-cached.  Bit-identical to recomputing the prefix: row
@@ -1333,6 +1381,22 @@ int capgen_debug_gemm(int M, int N, int K, const void* A, int64_t lda, int ta, c
     ga.M = M, ga.N = N, ga.K = K, ga.A = A, ga.lda = lda, ga.B = B, ga.ldb = ldb, ga.C = Cp, ga.ldc = ldc;
     ga.bias = bias, ga.alpha = alpha, ga.beta = beta, ga.relu = relu;
     gemm(ga, dt(in_dtype), dt(out_dtype), ta != 0, tb != 0, (hipStream_t)stream);
+  });
+}
+
+int capgen_rl_sample(capgen_t* h, const void* feats, int feats_dtype, const float* pos, const int32_t* caps, int B,
+                     int N, int T, int64_t* sample_out, float* entropy_out, float* lm_loss_out, void* stream) {
+  return guarded([&] {
+    set_device(h);
+    h->rl_sample(feats, dt(feats_dtype), pos, caps, B, N, T, sample_out, entropy_out, lm_loss_out, (hipStream_t)stream);
+  });
+}
+
+int capgen_rl_finish(capgen_t* h, const float* scores, float structure_loss_weight, float* loss_out, int train,
+                     void* stream) {
+  return guarded([&] {
+    set_device(h);
+    h->rl_finish(scores, structure_loss_weight, loss_out, train != 0, (hipStream_t)stream);
   });
 }
 

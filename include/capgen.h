@@ -125,6 +125,23 @@ int capgen_debug_gemm(int M, int N, int K, const void* A, int64_t lda, int ta, c
 /* Experiment hook: force a GEMM tile/wave/pipeline variant (0 = production heuristic). */
 int capgen_debug_gemm_variant(int variant);
 
+/* Self-critical sequence training (SelfCriticNetwork, models.py:137-211), in two calls with the
+ * host scoring the samples in between (CIDEr-D / BLEU, capgen/scst.py):
+ *  capgen_rl_sample  replaces PolicyNetwork.forward + .sample (model_RL.py:75-97) and the entropy
+ *                    of StructureCriterion (loss.py:123-127): teacher-forced forward (dropout as
+ *                    set by capgen_set_training), sample = argmax log_softmax [B, T-1] (int64),
+ *                    per-image masked mean entropy [B] and the CrossEntropy LM loss [1];
+ *  capgen_rl_finish  replaces ReinforcementLearningLoss.forward (loss.py:53-76, 131-152) and, when
+ *                    train != 0, loss.backward() + Adam.step() (models.py:191-195).  scores [B]
+ *                    (device) = per-image total score (cider_w*CIDEr-D + bleu_w*BLEU-4 +
+ *                    entropy_w*entropy + self_cider_w*self-CIDEr); loss_out [3] (device) =
+ *                    {loss, language_model_loss, structure_loss}.  Under DP, sum(mask) and the
+ *                    structure numerator are all-reduced (global mean as in one process). */
+int capgen_rl_sample(capgen_t* h, const void* feats, int feats_dtype, const float* pos, const int32_t* caps, int B,
+                     int N, int T, int64_t* sample_out, float* entropy_out, float* lm_loss_out, void* stream);
+int capgen_rl_finish(capgen_t* h, const float* scores, float structure_loss_weight, float* loss_out, int train,
+                     void* stream);
+
 /* Test hook: one masked multi-head attention forward (+ backward when dout != NULL) on packed
  * [B, L, H*dk] tensors (row stride H*dk), dtype 0 = f32, 1 = bf16 (the kernels the engine uses
  * for modules.py:16-27 ScaledDotProductAttention).  key_valid: optional [B][Lk] bytes (0 =

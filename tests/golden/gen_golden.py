@@ -135,6 +135,126 @@ def make_fixture(tag, cfg, B, N, T, seed, beam_k=5, min_valid=None):
     print(f"wrote {path}: loss={out['loss']:.6f} loss_after_step1={out['loss_after_step1']:.6f}")
 
 
+# ---- SCST (SelfCriticNetwork, models.py:137-211; model_RL.py:75-97; loss.py:31-220) -------
+# CIDEr-D / BLEU / self-CIDEr live in the un-vendored coco-caption code (core.metrics.*), so
+# the scorers are stubbed with INJECTED per-image scores (C5 parity is pinned
+# for the loss mechanics given reward vectors).  Weights: core/config.py:81-85.
+RL_WEIGHTS = dict(structure_loss_weight=0.5, cider_reward_weight=1.0, bleu_reward_weight=1.0,
+                  entropy_reward_weight=1.0, self_cider_reward_weight=1.0)
+
+
+def make_rl_fixture(tag, cfg, B, N, T, seed, min_valid=None, pad_frac=0.0):
+    """pad_frac > 0: raise the classifier bias of the pad id so that about that fraction of the
+    argmax samples are 0 (exercises the structure-loss mask; the boost is stored as
+    `pad_bias_boost` and applied to the fixture weights by the tests)."""
+    import pickle
+    import tempfile
+    import_reference()
+    rng = np.random.default_rng(seed + 7)
+    cider = rng.uniform(0.0, 2.0, size=B)
+    bleu = rng.uniform(0.0, 1.0, size=B)
+
+    class StubCiderD:
+        def __init__(self, df=None):
+            pass
+
+        def compute_score(self, gts, res):
+            assert len(res) == B
+            return float(cider.mean()), cider.copy()
+
+    class StubBleu:
+        def __init__(self, n=4, print_=False):
+            pass
+
+        def compute_score(self, gts, res):
+            return [0.0] * 4, [list(bleu) for _ in range(4)]
+
+    class StubCider:
+        def __init__(self, df=None):
+            pass
+
+        def my_self_cider(self, res):
+            return [np.array([[4.0]])]  # one caption per image: a 1x1 kernel -> diversity term 0
+
+    sys.modules["core.metrics.ciderD.ciderD"].CiderD = StubCiderD
+    sys.modules["core.metrics.bleu.bleu"].Bleu = StubBleu
+    sys.modules["core.metrics.cider.cider"].Cider = StubCider
+    for m in [k for k in list(sys.modules) if k.startswith("core.TRANSFORMER.loss")]:
+        del sys.modules[m]
+    from core.TRANSFORMER.loss import ReinforcementLearningLoss
+    from core.TRANSFORMER.model_RL import PolicyNetwork
+
+    torch.manual_seed(0)
+    model = PolicyNetwork(
+        num_vocab=cfg.num_vocab, max_length=cfg.max_length, encode_dim_positions=cfg.encode_dim_positions,
+        encode_dim_features=cfg.encode_dim_features, device="cpu", pad_idx=cfg.pad_idx, dropout=cfg.dropout,
+        encode_mask=cfg.encode_mask, encode_input_size=cfg.encode_input_size, encode_q_k_dim=cfg.encode_q_k_dim,
+        encode_v_dim=cfg.encode_v_dim, encode_hidden_size=cfg.encode_hidden_size,
+        encode_num_blocks=cfg.encode_num_blocks, encode_num_heads=cfg.encode_num_heads,
+        dim_word_embedding=cfg.dim_word_embedding, decode_input_size=cfg.decode_input_size,
+        decode_q_k_dim=cfg.decode_q_k_dim, decode_v_dim=cfg.decode_v_dim,
+        decode_hidden_size=cfg.decode_hidden_size, decode_num_blocks=cfg.decode_num_blocks,
+        decode_num_heads=cfg.decode_num_heads)
+    sd = {k: torch.from_numpy(v) for k, v in fixture_state_dict(cfg, seed=seed).items()}
+    model.load_state_dict(sd, strict=True)
+    model.eval()
+    feats, pos, caps = synthetic_batch(B, N, cfg.encode_dim_features, cfg.encode_dim_positions,
+                                       T, cfg.num_vocab, seed=seed + 100, min_valid=min_valid)
+    boost = 0.0
+    if pad_frac > 0:
+        with torch.no_grad():
+            lg = model(object_features=feats, position_features=pos, target_caption=caps)
+            gap = lg[..., 1:].max(-1).values - lg[..., 0]
+            boost = float(torch.quantile(gap.reshape(-1), pad_frac)) + 1e-3
+        sd["classifer.bias"] = sd["classifer.bias"].clone()
+        sd["classifer.bias"][0] += boost
+        model.load_state_dict(sd, strict=True)
+    vocab = {"<NULL>": 0, "<START>": 1, "<END>": 2}
+    vocab.update({f"w{i}": i for i in range(3, cfg.num_vocab)})
+    with tempfile.NamedTemporaryFile(suffix=".pkl", delete=False) as fh:
+        pickle.dump(vocab, fh)
+        vocab_path = fh.name
+    crit = ReinforcementLearningLoss(word_to_idx_path=vocab_path, pad_idx=cfg.pad_idx, **RL_WEIGHTS)
+    os.unlink(vocab_path)
+
+    out = {"feats": feats.numpy(), "pos": pos.numpy(), "caps": caps.numpy(),
+           "inj_cider": cider, "inj_bleu": bleu, "pad_bias_boost": np.float64(boost)}
+    for k, v in RL_WEIGHTS.items():
+        out[k] = np.float64(v)
+    logits = model(object_features=feats, position_features=pos, target_caption=caps)
+    seq, logp = model.sample(output=logits)
+    loss = crit(model_output=logits.cpu(), sample_sequence=seq.cpu(), sample_logprobs=logp.cpu(), target=caps)
+    loss["loss"].mean().backward()
+    out["loss"] = np.float64(loss["loss"].item())
+    out["language_model_loss"] = np.float64(loss["language_model_loss"].item())
+    out["structure_loss"] = np.float64(loss["structure_loss"].item())
+    out["reward"] = loss["reward"].detach().numpy().reshape(-1)
+    out["sample"] = seq.numpy()
+    names = [n for n, _ in reference_param_specs(cfg)]
+    params = dict(model.named_parameters())
+    gsum, gabs, gsamp = [], [], []
+    for n in names:
+        g = params[n].grad.detach().double().reshape(-1)
+        gsum.append(g.sum().item())
+        gabs.append(g.abs().sum().item())
+        gsamp.append(g[sample_index(n, g.numel())].numpy())
+    out["grad_sum"], out["grad_abs"] = np.array(gsum), np.array(gabs)
+    out["grad_samples"] = np.concatenate(gsamp)
+    out["seed"] = np.int64(seed)
+    out["cfg"] = np.array(repr(cfg))
+    path = os.path.join(HERE, f"{tag}.npz")
+    np.savez_compressed(path, **out)
+    print(f"wrote {path}: loss={out['loss']:.6f} lm={out['language_model_loss']:.6f} "
+          f"struct={out['structure_loss']:.6f}")
+
+
+RL_FIXTURES = {
+    # tag: (cfg, B, N, T, seed, min_valid, pad_frac)
+    "c5_rl": (preset("C1"), 8, 8, 10, 5, 4, 0.0),
+    "c5_rl_pad": (preset("C1"), 8, 8, 10, 6, 4, 0.35),
+}
+
+
 FIXTURES = {
     # tag: (cfg, B, N, T, seed, beam_k, min_valid)
     "c1": (preset("C1"), 8, 8, 10, 0, 5, 4),
@@ -150,6 +270,10 @@ def main(tags=None):
         if tags and tag not in tags:
             continue
         make_fixture(tag, cfg, B, N, T, seed, beam_k=k, min_valid=mv)
+    for tag, (cfg, B, N, T, seed, mv, pf) in RL_FIXTURES.items():
+        if tags and tag not in tags:
+            continue
+        make_rl_fixture(tag, cfg, B, N, T, seed, min_valid=mv, pad_frac=pf)
 
 
 if __name__ == "__main__":

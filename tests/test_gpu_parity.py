@@ -362,3 +362,58 @@ def test_attention_kernels_vs_torch(dtype, B, H, Lq, Lk, dk, causal, mask):
         ref = ref.detach().float()
         err = (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-6)
         assert err < tol, (name, err)
+
+
+def _rl_engine(tag, dtype="fp32"):
+    from capgen.engine import Engine
+    cfg, seed, z = load_fixture(tag)
+    sd = fixture_state_dict(cfg, seed=seed, with_buffer=False)
+    sd["classifer.bias"] = sd["classifer.bias"].copy()
+    sd["classifer.bias"][0] += float(z["pad_bias_boost"])
+    e = Engine(cfg.replace(dtype=dtype), DEV)
+    e.load_state_dict(sd)
+    e.set_training(False)
+    base = float(z["cider_reward_weight"]) * z["inj_cider"] + float(z["bleu_reward_weight"]) * z["inj_bleu"]
+    return cfg, e, z, base
+
+
+@pytest.mark.parametrize("tag", ["c5_rl", "c5_rl_pad"])
+def test_scst_step_matches_reference(tag):
+    """SelfCriticNetwork mechanics through the C ABI (rl_sample -> host reward -> rl_finish) vs the
+    reference's ReinforcementLearningLoss with the same injected CIDEr-D / BLEU scores: samples
+    bit-exact, loss / LM / structure loss within 1e-3, gradients as in the CE tests."""
+    cfg, e, z, base = _rl_engine(tag)
+    f, p, c = _inputs(z)
+    seq, ent, lm = e.rl_sample(f, p, c)
+    assert (seq.cpu().numpy() == z["sample"]).all()
+    total = base + float(z["entropy_reward_weight"]) * ent.cpu().double().numpy()
+    out = e.rl_finish(total, float(z["structure_loss_weight"]), train=True).cpu()
+    for i, k in enumerate(("loss", "language_model_loss", "structure_loss")):
+        assert abs(out[i].item() - float(z[k])) < 1e-3 * max(1.0, abs(float(z[k]))), (k, out[i].item(), float(z[k]))
+    g = e.grads_state_dict()
+    names = [n for n, _ in reference_param_specs(cfg)]
+    samples = []
+    for i, n in enumerate(names):
+        gi = g[n].double().reshape(-1)
+        ref = float(z["grad_abs"][i])
+        assert abs(gi.abs().sum().item() - ref) <= 1e-3 * ref + 1e-6, (n, gi.abs().sum().item(), ref)
+        samples.append(gi[sample_index(n, gi.numel())].numpy())
+    ref = z["grad_samples"]
+    np.testing.assert_allclose(np.concatenate(samples), ref, atol=1e-4 + 1e-3 * np.abs(ref).max(), rtol=1e-2)
+
+
+def test_scst_compute_loss_has_no_side_effects_and_bf16_close():
+    cfg, e, z, base = _rl_engine("c5_rl_pad")
+    f, p, c = _inputs(z)
+    before = e.state_dict(with_buffer=False)
+    seq, ent, _ = e.rl_sample(f, p, c)
+    total = base + ent.cpu().double().numpy()
+    out = e.rl_finish(total, 0.5, train=False).cpu()
+    after = e.state_dict(with_buffer=False)
+    for k in before:
+        assert torch.equal(before[k], after[k]), k
+    assert abs(out[0].item() - float(z["loss"])) < 1e-3 * abs(float(z["loss"]))
+    _, eb, _, _ = _rl_engine("c5_rl_pad", dtype="bf16")
+    seqb, entb, _ = eb.rl_sample(f, p, c)
+    outb = eb.rl_finish(base + entb.cpu().double().numpy(), 0.5, train=False).cpu()
+    assert abs(outb[0].item() - float(z["loss"])) < 3e-2 * abs(float(z["loss"]))

@@ -74,3 +74,33 @@ def test_masks_fire_in_fixtures():
         _, _, z = load_fixture(tag)
         assert (np.count_nonzero(z["pos"], axis=2) == 0).any(), tag
         assert (z["caps"] == 0).any(), tag
+
+
+def rl_setup(tag):
+    """SCST fixtures: fixture weights (+ the pad-id bias boost the generator applied)."""
+    cfg, seed, z = load_fixture(tag)
+    sd = fixture_state_dict(cfg, seed=seed, with_buffer=False)
+    sd["classifer.bias"] = sd["classifer.bias"].copy()
+    sd["classifer.bias"][0] += float(z["pad_bias_boost"])
+    x = [torch.from_numpy(z[k]) for k in ("feats", "pos", "caps")]
+    base = float(z["cider_reward_weight"]) * z["inj_cider"] + float(z["bleu_reward_weight"]) * z["inj_bleu"]
+    return cfg, sd, x, z, base
+
+
+@pytest.mark.parametrize("tag", ["c5_rl", "c5_rl_pad"])
+def test_rl_loss_and_grads(tag):
+    """SelfCriticNetwork step mechanics (model_RL.py:75-97, loss.py:31-220) with injected rewards."""
+    cfg, sd, (f, p, c), z, base = rl_setup(tag)
+    P = O.make_params(sd)
+    logits = O.forward_logits(P, cfg, f, p, c, training=False)
+    out = O.rl_loss_from_logits(logits, c, base, float(z["structure_loss_weight"]),
+                                float(z["entropy_reward_weight"]), float(z["self_cider_reward_weight"]))
+    assert (out["sample"].numpy() == z["sample"]).all()
+    np.testing.assert_allclose(out["reward"].numpy(), z["reward"], rtol=1e-6)
+    for k in ("loss", "language_model_loss", "structure_loss"):
+        assert abs(out[k].item() - float(z[k])) < 1e-4 * max(1.0, abs(float(z[k]))), k
+    out["loss"].backward()
+    names = [n for n, _ in reference_param_specs(cfg)]
+    for i, n in enumerate(names):
+        g = P[n].grad.double().reshape(-1)
+        assert abs(g.abs().sum().item() - z["grad_abs"][i]) <= 1e-4 * max(1.0, z["grad_abs"][i]), n
