@@ -67,6 +67,8 @@ _SIGS = {
     "capgen_debug_gemm": (C.c_int, [C.c_int, C.c_int, C.c_int, _P, C.c_int64, C.c_int, _P, C.c_int64, C.c_int,
                                     _P, C.c_int64, C.c_int, C.c_int, _P, C.c_float, C.c_int, C.c_int, _P]),
     "capgen_debug_gemm_variant": (C.c_int, [C.c_int]),
+    "capgen_train_step_indexed": (C.c_int, [_P, _P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int, _P,
+                                            _P]),
     "capgen_rl_sample": (C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P]),
     "capgen_rl_finish": (C.c_int, [_P, _P, C.c_float, _P, C.c_int, _P]),
     "capgen_debug_attention": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P,

@@ -163,6 +163,21 @@ class Engine:
         _lib.check(self.lib.capgen_train_step(self.h, _ptr(f), ft, _ptr(p), _ptr(c), B, N, T, _ptr(out),
                                               _stream(self.device)))
 
+    def train_step_indexed(self, feat_store, pos_store, img_idx, caps, out=None):
+        """Training step reading features of images img_idx[b] from device-resident stores
+        (capgen.data.DeviceFeatureStore): no per-step host->device copy of features."""
+        assert feat_store.is_cuda and pos_store.is_cuda and img_idx.is_cuda and caps.is_cuda
+        assert feat_store.dim() == 3 and pos_store.shape[:2] == feat_store.shape[:2]
+        ft = _lib.BF16 if feat_store.dtype == torch.bfloat16 else _lib.F32
+        idx = img_idx.to(torch.int32).contiguous()
+        c = caps.to(torch.int32).contiguous()
+        B, T = c.shape
+        out = self._loss if out is None else out
+        _lib.check(self.lib.capgen_train_step_indexed(self.h, _ptr(feat_store), ft, _ptr(pos_store),
+                                                      feat_store.shape[0], _ptr(idx), _ptr(c), B,
+                                                      feat_store.shape[1], T, _ptr(out), _stream(self.device)))
+        return out
+
     def compute_loss(self, feats, pos, caps):
         out = torch.zeros(1, dtype=torch.float32, device=self.device)
         f, ft, p, c = self._inputs(feats, pos, caps)

@@ -83,6 +83,11 @@ class TRANSFORMER(MODEL_init):
         c = self._staged("c", batch_captions, torch.int32)
         self.model.engine.train_step(f, p, c)
 
+    def train_step_resident(self, store, img_idx, captions):
+        """train_step over an HBM-resident split (capgen.data.DeviceFeatureStore / ResidentBatches):
+        the batch names its images; nothing is copied from the host."""
+        self.model.engine.train_step_indexed(store.features, store.positions, img_idx, captions)
+
     def compute_loss(self, object_features, position_features, target_caption):
         """models.py:128-135 (no_grad; dropout follows train/eval state)."""
         with torch.no_grad():

@@ -223,9 +223,11 @@ struct capgen_engine {
     float* loss;
     int ft, B, N, T;
     bool drop;
+    const void* idx;
+    int nimg;
     bool operator==(const Key& o) const {
       return f == o.f && p == o.p && c == o.c && loss == o.loss && ft == o.ft && B == o.B && N == o.N && T == o.T &&
-             drop == o.drop;
+             drop == o.drop && idx == o.idx && nimg == o.nimg;
     }
   } gkey{};
   std::vector<std::array<int, 3>> tuned_shapes;
@@ -433,7 +435,7 @@ struct capgen_engine {
     const float p = cfg.dropout, pa = cfg.attention_dropout;
     if (drop_on) bump_seed(seed, s);
 
-    pack_encoder_input(feats, ft, pos, Me, L.F, L.P, L.Kp, a.Aenc, act, a.valid, s);
+    pack_encoder_input(feats, ft, pos, Me, L.F, L.P, L.Kp, a.Aenc, act, a.valid, s, in_idx, N, in_n_img);
     prepare_captions(caps, B, T, cfg.pad_idx, a.ids, a.tgt, a.count, s);
     if (comm) {
       if (count_override)
@@ -781,7 +783,7 @@ struct capgen_engine {
                   hipStream_t cs) {
     ensure_acts(B, N, T);
     enter(cs);
-    Key k{f, pos, caps, loss, (int)ft, B, N, T, training};
+    Key k{f, pos, caps, loss, (int)ft, B, N, T, training, in_idx, in_n_img};
     auto body = [&]() {
       forward(f, ft, pos, caps, B, N, T, loss, training, es);
       backward(es, /*step_params=*/true);  // + bucketed RCCL all-reduce (DP) and Adam
@@ -854,6 +856,9 @@ struct capgen_engine {
     leave(cs);
   }
   int rl_B = 0;
+  // resident feature store: when set, forward() gathers image in_idx[b] from feats/pos
+  const int32_t* in_idx = nullptr;
+  int in_n_img = 0;
 
   // ------------------------------------------------------------------------------------
   // decoding (model.py:101-200), KV-cached.  Bit-identical to recomputing the prefix: row
@@ -1381,6 +1386,24 @@ int capgen_debug_gemm(int M, int N, int K, const void* A, int64_t lda, int ta, c
     ga.M = M, ga.N = N, ga.K = K, ga.A = A, ga.lda = lda, ga.B = B, ga.ldb = ldb, ga.C = Cp, ga.ldc = ldc;
     ga.bias = bias, ga.alpha = alpha, ga.beta = beta, ga.relu = relu;
     gemm(ga, dt(in_dtype), dt(out_dtype), ta != 0, tb != 0, (hipStream_t)stream);
+  });
+}
+
+int capgen_train_step_indexed(capgen_t* h, const void* feat_store, int feats_dtype, const float* pos_store,
+                              int n_images, const int32_t* img_idx, const int32_t* caps, int B, int N, int T,
+                              float* loss_out, void* stream) {
+  return guarded([&] {
+    set_device(h);
+    require(n_images >= 1, "train_step_indexed: empty store");
+    h->in_idx = img_idx;
+    h->in_n_img = n_images;
+    try {
+      h->train_step(feat_store, dt(feats_dtype), pos_store, caps, B, N, T, loss_out, (hipStream_t)stream);
+    } catch (...) {
+      h->in_idx = nullptr;
+      throw;
+    }
+    h->in_idx = nullptr;
   });
 }
 

@@ -55,8 +55,11 @@ struct LnBwd {
 void layernorm_bwd(const LnBwd& a, DType t, hipStream_t s);
 
 // out[m] = [feats[m] | pos[m] | 0] (width Kp), valid[m] = any(pos[m] != 0)  (model.py:202-209)
+// img_idx (optional, [M/N]): rows of image img_idx[b] of a resident [n_img, N, F] / [.., P] store
+// (indices outside [0, n_img) give all-padding rows)
 void pack_encoder_input(const void* feats, DType feats_t, const float* pos, int M, int F, int P, int Kp,
-                        void* out, DType out_t, uint8_t* valid, hipStream_t s);
+                        void* out, DType out_t, uint8_t* valid, hipStream_t s, const int32_t* img_idx = nullptr,
+                        int N = 0, int n_img = 0);
 // caps [B][T] -> ids_in [B][T-1], tgt [B][T-1]; count = #(tgt != pad) as f32   (model.py:88-89)
 void prepare_captions(const int32_t* caps, int B, int T, int pad, int32_t* ids_in, int32_t* tgt,
                       float* count, hipStream_t s);

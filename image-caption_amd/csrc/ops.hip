@@ -198,22 +198,44 @@ void layernorm_bwd(const LnBwd& a, DType t, hipStream_t s) {
 
 // ---------------------------------------------------------------------------------------
 template <typename TI, typename TO>
-__global__ void pack_kernel(const TI* __restrict__ feats, const float* __restrict__ pos, int F, int P, int Kp,
-                            TO* __restrict__ out, uint8_t* __restrict__ valid) {
+__global__ void __launch_bounds__(256) pack_kernel(const TI* __restrict__ feats, const float* __restrict__ pos,
+                                                   const int32_t* __restrict__ img_idx, int n_img, int N, int F, int P,
+                                                   int Kp, TO* __restrict__ out, uint8_t* __restrict__ valid) {
+  constexpr int V = 16 / sizeof(TI);  // one 16-B load of features per step
   __shared__ int nz;
   const int m = blockIdx.x;
+  // row m = (b, n) of the batch; with img_idx the features / positions of image img_idx[b] are
+  // read straight from an HBM-resident store (dataset.py:12-18 + DataLoader collate, fused)
+  int64_t src = m;
+  if (img_idx) {
+    const int img = img_idx[m / N];
+    if (img < 0 || img >= n_img) {  // out-of-range image: an all-padding row, never an OOB read
+      for (int c = threadIdx.x; c < Kp; c += 256) out[(int64_t)m * Kp + c] = from_f<TO>(0.f);
+      if (threadIdx.x == 0) valid[m] = 0;
+      return;
+    }
+    src = (int64_t)img * N + m % N;
+  }
   if (threadIdx.x == 0) nz = 0;
   __syncthreads();
-  const TI* f = feats + (int64_t)m * F;
-  const float* p = pos + (int64_t)m * P;
+  const TI* f = feats + src * F;
+  const float* p = pos + src * P;
   TO* o = out + (int64_t)m * Kp;
-  for (int c = threadIdx.x; c < Kp; c += blockDim.x) {
-    float x;
-    if (c < F) x = to_f(f[c]);
-    else if (c < F + P) {
+  for (int c = threadIdx.x * V; c < F; c += 256 * V) {
+    typedef typename Vec16<TI>::type VT;
+    const VT v = *reinterpret_cast<const VT*>(f + c);
+    const TI* e = reinterpret_cast<const TI*>(&v);
+    float x[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) x[j] = to_f(e[j]);
+    store_f<TO, V>(o + c, x);
+  }
+  for (int c = F + threadIdx.x; c < Kp; c += 256) {
+    float x = 0.f;
+    if (c < F + P) {
       x = p[c - F];
       if (x != 0.f) atomicOr(&nz, 1);
-    } else x = 0.f;
+    }
     o[c] = from_f<TO>(x);
   }
   __syncthreads();
@@ -221,17 +243,19 @@ __global__ void pack_kernel(const TI* __restrict__ feats, const float* __restric
 }
 
 void pack_encoder_input(const void* feats, DType ft, const float* pos, int M, int F, int P, int Kp, void* out,
-                        DType ot, uint8_t* valid, hipStream_t s) {
+                        DType ot, uint8_t* valid, hipStream_t s, const int32_t* img_idx, int N, int n_img) {
   if (M <= 0) return;
+  require(F % 8 == 0 && ((uintptr_t)feats & 15) == 0, "pack: feature width must be a multiple of 8, 16-B aligned");
+  require(img_idx == nullptr || N > 0, "pack: indexed gather needs N");
   dim3 grid(M);
   if (ft == DType::F32 && ot == DType::F32)
-    pack_kernel<float, float><<<grid, 256, 0, s>>>((const float*)feats, pos, F, P, Kp, (float*)out, valid);
+    pack_kernel<float, float><<<grid, 256, 0, s>>>((const float*)feats, pos, img_idx, n_img, N, F, P, Kp, (float*)out, valid);
   else if (ft == DType::F32 && ot == DType::BF16)
-    pack_kernel<float, bf16><<<grid, 256, 0, s>>>((const float*)feats, pos, F, P, Kp, (bf16*)out, valid);
+    pack_kernel<float, bf16><<<grid, 256, 0, s>>>((const float*)feats, pos, img_idx, n_img, N, F, P, Kp, (bf16*)out, valid);
   else if (ft == DType::BF16 && ot == DType::BF16)
-    pack_kernel<bf16, bf16><<<grid, 256, 0, s>>>((const bf16*)feats, pos, F, P, Kp, (bf16*)out, valid);
+    pack_kernel<bf16, bf16><<<grid, 256, 0, s>>>((const bf16*)feats, pos, img_idx, n_img, N, F, P, Kp, (bf16*)out, valid);
   else
-    pack_kernel<bf16, float><<<grid, 256, 0, s>>>((const bf16*)feats, pos, F, P, Kp, (float*)out, valid);
+    pack_kernel<bf16, float><<<grid, 256, 0, s>>>((const bf16*)feats, pos, img_idx, n_img, N, F, P, Kp, (float*)out, valid);
   CAPGEN_HIP(hipGetLastError());
 }
 

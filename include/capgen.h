@@ -125,6 +125,15 @@ int capgen_debug_gemm(int M, int N, int K, const void* A, int64_t lda, int ta, c
 /* Experiment hook: force a GEMM tile/wave/pipeline variant (0 = production heuristic). */
 int capgen_debug_gemm_variant(int variant);
 
+/* Training step over an HBM-resident feature store (replaces TrainDataset.__getitem__ + the
+ * DataLoader collate + `.to(DEVICE)`, dataset.py:12-18, main.py:37-43, models.py:120-122):
+ * feat_store [n_images, N, F] and pos_store [n_images, N, P] stay on the device (a COCO split in
+ * bf16 is ~17 GB); img_idx [B] (device int32) selects each caption's image, gathered inside the
+ * encoder-input pack kernel; caps [B, T] device int32.  Otherwise as capgen_train_step. */
+int capgen_train_step_indexed(capgen_t* h, const void* feat_store, int feats_dtype, const float* pos_store,
+                              int n_images, const int32_t* img_idx, const int32_t* caps, int B, int N, int T,
+                              float* loss_out, void* stream);
+
 /* Self-critical sequence training (SelfCriticNetwork, models.py:137-211), in two calls with the
  * host scoring the samples in between (CIDEr-D / BLEU, capgen/scst.py):
  *  capgen_rl_sample  replaces PolicyNetwork.forward + .sample (model_RL.py:75-97) and the entropy
