@@ -68,13 +68,15 @@ elif __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "one":
     run(M, N, K, ta, tb, f32)
 elif __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "sk":
     # split-K study: eager launches (the split-K workspace is per stream), event timing
-    for (M, N, K, ta, tb, f32) in [(512, 512, 2304, 1, 1, 1), (2048, 512, 2304, 1, 1, 1), (2304, 512, 2048, 0, 0, 0),
-                                   (2304, 512, 2048, 0, 1, 0), (1216, 512, 10000, 0, 1, 0)]:
+    shapes = [(512, 512, 2304, 1, 1, 1), (2048, 512, 2304, 1, 1, 1), (2304, 512, 2048, 0, 0, 0),
+              (2304, 512, 2048, 0, 1, 0), (1216, 512, 10000, 0, 1, 0)]
+    variants = (6, 12, 13, 14, 8)
+    for (M, N, K, ta, tb, f32) in shapes:
         A = torch.randn((K, M) if ta else (M, K), device="cuda", dtype=torch.bfloat16)
         B = torch.randn((K, N) if tb else (N, K), device="cuda", dtype=torch.bfloat16)
         Cc = torch.empty(M, N, device="cuda", dtype=torch.float32 if f32 else torch.bfloat16)
         ref = None
-        for v in (6, 12, 13, 14, 8):
+        for v in variants:
             for sk in (1, 2, 3, 4, 6):
                 _lib.check(lib.capgen_debug_gemm_variant(v + 100 * sk))
                 s = torch.cuda.current_stream()
