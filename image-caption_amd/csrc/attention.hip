@@ -222,6 +222,61 @@ __global__ void __launch_bounds__(AT_THREADS) attn_bwd_kernel(AttnGeom g, const 
   }
 }
 
+// Single-query attention (KV-cached decode step, model.py:101-200 with a cache): one wave64 per
+// (row, head), lane = key for the scores / softmax and lane = head dim for P.V.  Every sum runs in
+// the same order as attn_fwd_kernel (q / temperature first; d-sequential dots; the same wave
+// butterflies; j-sequential P.V), so f32 results are bit-identical to it.  No dropout (decode).
+template <typename T>
+__global__ void __launch_bounds__(256) attn_decode_kernel(AttnGeom g, T* __restrict__ o, float* __restrict__ probs) {
+  __shared__ float qsh[4][64];
+  __shared__ T vsh[4][64 * 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int w = blockIdx.x * 4 + wv;
+  const bool live = w < g.B * g.H;
+  const int b = live ? w / g.H : 0, h = live ? w % g.H : 0;
+  const int bk = g.kv_bmod ? b % g.kv_bmod : b;
+  const T* q = reinterpret_cast<const T*>(g.q) + (int64_t)b * g.q_bs + h * 64;
+  const T* kb = reinterpret_cast<const T*>(g.k) + (int64_t)bk * g.k_bs + h * 64;
+  const T* vb = reinterpret_cast<const T*>(g.v) + (int64_t)bk * g.v_bs + h * 64;
+  // stage q / temperature (lane = dim) and the V rows (coalesced 16-B chunks) in LDS
+  constexpr int V = 16 / sizeof(T);
+  typedef typename Vec16<T>::type VT;
+  if (live) {
+    qsh[wv][lane] = to_f(q[lane]) / g.temperature;
+    for (int c = lane; c < g.Lk * (64 / V); c += 64) {
+      const int jj = c / (64 / V), d0 = (c % (64 / V)) * V;
+      *reinterpret_cast<VT*>(&vsh[wv][jj * 64 + d0]) = *reinterpret_cast<const VT*>(vb + (int64_t)jj * g.v_ld + d0);
+    }
+  }
+  __syncthreads();
+  if (!live) return;
+  const int j = lane;
+  float s = -INFINITY;
+  if (j < g.Lk && !key_masked(g, b, 0, j)) {
+    const T* kr = kb + (int64_t)j * g.k_ld;
+    float kx[64];
+#pragma unroll
+    for (int d0 = 0; d0 < 64; d0 += V) {
+      float t[V];
+      load_f<T, V>(kr + d0, t);
+#pragma unroll
+      for (int e = 0; e < V; ++e) kx[d0 + e] = t[e];
+    }
+    float acc = 0.f;
+#pragma unroll
+    for (int d = 0; d < 64; ++d) acc = fmaf(qsh[wv][d], kx[d], acc);
+    s = acc;
+  }
+  const float mx = wave_max(s);
+  const float e = j < g.Lk ? expf(s - mx) : 0.f;
+  const float sum = wave_sum(e);
+  const float p = e / sum;
+  if (probs && j < g.Lk) probs[(((int64_t)b * g.H + h)) * g.Lk + j] = p;
+  float acc = 0.f;
+  for (int jj = 0; jj < g.Lk; ++jj) acc = fmaf(__shfl(p, jj, 64), to_f(vsh[wv][jj * 64 + lane]), acc);
+  o[(int64_t)b * g.o_bs + h * 64 + lane] = from_f<T>(acc);
+}
+
 __global__ void head_mean_kernel(const float* __restrict__ probs, int B, int H, int Lq, int Lk, int row,
                                  float* __restrict__ out) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -257,6 +312,14 @@ static void allow_big_lds(K kernel) {
 
 void attention_fwd(const AttnGeom& g, void* o, float* probs, DType t, hipStream_t s) {
   check_geom(g);
+  if (g.Lq == 1 && g.dk == 64 && g.drop.seed_ptr == nullptr && g.q_ld % 8 == 0 && g.k_ld % 8 == 0 &&
+      ((g.q_bs | g.k_bs) % 8) == 0) {  // KV-cached decode step
+    const int blocks = (g.B * g.H + 3) / 4;
+    if (t == DType::F32) attn_decode_kernel<float><<<blocks, 256, 0, s>>>(g, (float*)o, probs);
+    else attn_decode_kernel<bf16><<<blocks, 256, 0, s>>>(g, (bf16*)o, probs);
+    CAPGEN_HIP(hipGetLastError());
+    return;
+  }
   if (t == DType::BF16 && attention_mfma_ok(g)) return attention_fwd_mfma(g, (bf16*)o, probs, s);
   const size_t smem = fwd_smem(g);
   require(smem <= 160 * 1024, "attention_fwd: LDS budget exceeded");

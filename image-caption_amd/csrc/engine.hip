@@ -114,58 +114,84 @@ __global__ void init_gen_ids_kernel(int64_t* out, int rows, int width, int32_t* 
 }
 
 // one workgroup per image: top-k (descending, lowest index first on ties) over the k*V
-// candidates probs[j*B+i][v] + prob[j][i]   (model.py:183-190)
+// candidates probs[j*B+i][v] + prob[j][i]   (model.py:183-190).  One pass: every thread keeps a
+// sorted register top-KM of its strided candidates, then the block merges the 256 * KM
+// finalists in LDS (k rounds of a block argmax over <= 4096 entries).  (value desc, index asc)
+// is a strict total order, so the selection equals a full sort's first k.
+template <int KM>
 __global__ void __launch_bounds__(256) beam_topk_kernel(const float* __restrict__ probs, const float* __restrict__ prev,
                                                         int k_in, int B, int V, int k, float* __restrict__ out_prob,
                                                         int32_t* __restrict__ out_src, int32_t* __restrict__ out_tok) {
+  __shared__ float fv[256 * KM];
+  __shared__ int fi[256 * KM];
   __shared__ float bv[4];
-  __shared__ int bi[4];
-  __shared__ int chosen[16];
-  const int i = blockIdx.x;
-  const int total = k_in * V;
+  __shared__ int bi[4], bp[4];
+  const int i = blockIdx.x, tid = threadIdx.x;
+  float tv[KM];
+  int ti[KM];
+#pragma unroll
+  for (int u = 0; u < KM; ++u) tv[u] = -INFINITY, ti[u] = 0x7fffffff;
+  for (int j = 0; j < k_in; ++j) {
+    const float* row = probs + ((int64_t)j * B + i) * V;
+    const float add = prev ? prev[j * B + i] : 0.f;
+    for (int v = tid; v < V; v += 256) {
+      const float x = row[v] + add;
+      const int c = j * V + v;
+      if (!(x > tv[KM - 1] || (x == tv[KM - 1] && c < ti[KM - 1]))) continue;
+      // insert into the sorted register list (unrolled: no dynamic register indexing)
+      float cv = x;
+      int ci = c;
+#pragma unroll
+      for (int u = 0; u < KM; ++u) {
+        const bool better = cv > tv[u] || (cv == tv[u] && ci < ti[u]);
+        const float ov = tv[u];
+        const int oi = ti[u];
+        tv[u] = better ? cv : ov;
+        ti[u] = better ? ci : oi;
+        cv = better ? ov : cv;
+        ci = better ? oi : ci;
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < KM; ++u) fv[u * 256 + tid] = tv[u], fi[u * 256 + tid] = ti[u];
+  __syncthreads();
   for (int sel = 0; sel < k; ++sel) {
     float best = -INFINITY;
-    int bidx = 0x7fffffff;
-    for (int c = threadIdx.x; c < total; c += 256) {
-      bool used = false;
-      for (int u = 0; u < sel; ++u) used |= (chosen[u] == c);
-      if (used) continue;
-      const int j = c / V, v = c % V;
-      const float x = probs[((int64_t)j * B + i) * V + v] + (prev ? prev[j * B + i] : 0.f);
-      if (x > best || (x == best && c < bidx)) {
-        best = x;
-        bidx = c;
-      }
+    int bidx = 0x7fffffff, bpos = -1;
+    for (int e = tid; e < 256 * KM; e += 256) {
+      const float x = fv[e];
+      const int c = fi[e];
+      if (x > best || (x == best && c < bidx)) best = x, bidx = c, bpos = e;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-      float ov = __shfl_xor(best, o, 64);
-      int oi = __shfl_xor(bidx, o, 64);
-      if (ov > best || (ov == best && oi < bidx)) {
-        best = ov;
-        bidx = oi;
-      }
+      const float ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bidx, o, 64);
+      const int op = __shfl_xor(bpos, o, 64);
+      if (ov > best || (ov == best && oi < bidx)) best = ov, bidx = oi, bpos = op;
     }
-    if ((threadIdx.x & 63) == 0) {
-      bv[threadIdx.x >> 6] = best;
-      bi[threadIdx.x >> 6] = bidx;
-    }
+    if ((tid & 63) == 0) bv[tid >> 6] = best, bi[tid >> 6] = bidx, bp[tid >> 6] = bpos;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      best = bv[0];
-      bidx = bi[0];
+    if (tid == 0) {
+      int w0 = 0;
       for (int w = 1; w < 4; ++w)
-        if (bv[w] > best || (bv[w] == best && bi[w] < bidx)) {
-          best = bv[w];
-          bidx = bi[w];
-        }
-      chosen[sel] = bidx;
-      out_prob[sel * B + i] = best;
-      out_src[sel * B + i] = bidx / V;
-      out_tok[sel * B + i] = bidx % V;
+        if (bv[w] > bv[w0] || (bv[w] == bv[w0] && bi[w] < bi[w0])) w0 = w;
+      out_prob[sel * B + i] = bv[w0];
+      out_src[sel * B + i] = bi[w0] / V;
+      out_tok[sel * B + i] = bi[w0] % V;
+      if (bp[w0] >= 0) fv[bp[w0]] = -INFINITY, fi[bp[w0]] = 0x7fffffff;
     }
     __syncthreads();
   }
+}
+
+static void beam_topk(const float* probs, const float* prev, int k_in, int B, int V, int k, float* out_prob,
+                      int32_t* out_src, int32_t* out_tok, hipStream_t s) {
+  if (k <= 4) beam_topk_kernel<4><<<B, 256, 0, s>>>(probs, prev, k_in, B, V, k, out_prob, out_src, out_tok);
+  else if (k <= 8) beam_topk_kernel<8><<<B, 256, 0, s>>>(probs, prev, k_in, B, V, k, out_prob, out_src, out_tok);
+  else beam_topk_kernel<16><<<B, 256, 0, s>>>(probs, prev, k_in, B, V, k, out_prob, out_src, out_tok);
+  CAPGEN_HIP(hipGetLastError());
 }
 
 // dst row r = (j, i) <- src row (src[j][i], i); then optionally set column `col` to tok
@@ -179,6 +205,17 @@ __global__ void beam_gather_kernel(const E* __restrict__ src, E* __restrict__ ds
   E* d = dst + (int64_t)r * row_elems;
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < copy_elems; c += (int64_t)gridDim.x * blockDim.x)
     d[c] = (tok && c == col) ? (E)tok[r] : s[c];
+}
+
+// the KV-cache rows of beam reorder: 16-B copies (row_elems, copy_elems multiples of 16 B)
+__global__ void beam_gather16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t row_vec,
+                                     int64_t copy_vec, const int32_t* __restrict__ bsrc, int B) {
+  const int r = blockIdx.y;
+  const int srow = bsrc[r] * B + (r % B);
+  const uint4* s = src + (int64_t)srow * row_vec;
+  uint4* d = dst + (int64_t)r * row_vec;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < copy_vec; c += (int64_t)gridDim.x * blockDim.x)
+    d[c] = s[c];
 }
 
 }  // namespace
@@ -1027,8 +1064,7 @@ struct capgen_engine {
     // position 0: every beam holds <START>; top-k of beam 0's distribution (model.py:148-166)
     dec_step(R, B, N, 0, g.cache, g.ids, false, s);
     softmax_rows(g.logits, R, L.V, g.probs, s);
-    beam_topk_kernel<<<B, 256, 0, s>>>(g.probs, nullptr, 1, B, L.V, k, g.bprob, g.bsrc, g.btok);
-    CAPGEN_HIP(hipGetLastError());
+    beam_topk(g.probs, nullptr, 1, B, L.V, k, g.bprob, g.bsrc, g.btok, s);
     CAPGEN_HIP(hipMemsetAsync(g.bsrc, 0, sizeof(int32_t) * R, s));  // all beams descend from beam 0 at t = 0
     auto reorder = [&](int t) {
       // seq/ids rows follow their source beam, then column t+1 = chosen token
@@ -1036,16 +1072,11 @@ struct capgen_engine {
       beam_gather_kernel<int64_t><<<gs, 64, 0, s>>>(g.seq, g.seq2, Tw, Tw, g.bsrc, B, R, g.btok, t + 1);
       beam_gather_kernel<int32_t><<<gs, 64, 0, s>>>(g.ids, g.ids2, Tc, Tc, g.bsrc, B, R, g.btok, t + 1);
       const int64_t cld = (int64_t)Tc * 2 * dd;
+      const int64_t vec_per_row = cld * (int64_t)es_() / 16, copy_vec = (int64_t)(t + 1) * 2 * dd * es_() / 16;
       for (int l = 0; l < L.Ld; ++l) {
-        dim3 gc(std::min<int64_t>(((int64_t)(t + 1) * 2 * dd + 255) / 256, 64), R);
-        if (act == DType::F32)
-          beam_gather_kernel<float><<<gc, 256, 0, s>>>((const float*)at(g.cache, l * R * cld),
-                                                       (float*)at(g.cache2, l * R * cld), cld, (int64_t)(t + 1) * 2 * dd,
-                                                       g.bsrc, B, R, nullptr, 0);
-        else
-          beam_gather_kernel<bf16><<<gc, 256, 0, s>>>((const bf16*)at(g.cache, l * R * cld),
-                                                      (bf16*)at(g.cache2, l * R * cld), cld, (int64_t)(t + 1) * 2 * dd,
-                                                      g.bsrc, B, R, nullptr, 0);
+        dim3 gc((unsigned)std::min<int64_t>((copy_vec + 255) / 256, 64), R);
+        beam_gather16_kernel<<<gc, 256, 0, s>>>((const uint4*)at(g.cache, l * R * cld), (uint4*)at(g.cache2, l * R * cld),
+                                                vec_per_row, copy_vec, g.bsrc, B);
       }
       CAPGEN_HIP(hipGetLastError());
       std::swap(g.seq, g.seq2);
@@ -1056,8 +1087,7 @@ struct capgen_engine {
     for (int t = 1; t < Tw - 1; ++t) {
       dec_step(R, B, N, t, g.cache, g.ids, false, s);
       softmax_rows(g.logits, R, L.V, g.probs, s);
-      beam_topk_kernel<<<B, 256, 0, s>>>(g.probs, g.bprob, k, B, L.V, k, g.bprob2, g.bsrc, g.btok);
-      CAPGEN_HIP(hipGetLastError());
+      beam_topk(g.probs, g.bprob, k, B, L.V, k, g.bprob2, g.bsrc, g.btok, s);
       std::swap(g.bprob, g.bprob2);
       reorder(t);
     }

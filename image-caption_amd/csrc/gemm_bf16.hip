@@ -27,6 +27,8 @@
 //
 // Tiles BMxBNx64, 256 threads = 2x2 wave64s; blocks remapped so consecutive tiles (sharing
 // an A row-panel) land on the same XCD L2.
+#include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <map>
@@ -153,7 +155,7 @@ __device__ __forceinline__ void store4(TO* p, const float (&v)[4]) {
 template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int STAGES>
 __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmArgs g, int tiles_n, int nblk,
                                                                 const void* zero, int splitk, float* ws,
-                                                                int* tile_cnt) {
+                                                                int* tile_cnt, int group_m) {
   constexpr int NW = WM * WN;
   typedef Op<TA, BM, NW> OA;
   typedef Op<TB, BN, NW> OB;
@@ -169,7 +171,15 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmArgs g, int
   const int xcd = bid & 7, q8 = nblk >> 3, r8 = nblk & 7;
   const int slot = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int tile = slot / splitk, split = slot % splitk;  // split-K slices of a tile are adjacent
-  const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
+  // tiles in column-major groups of group_m tile rows: an XCD's contiguous slot range covers a
+  // compact 2D block of the output (fewer distinct A row panels + B column panels per L2)
+  int mt = tile / tiles_n, nt = tile % tiles_n;
+  if (group_m > 1) {
+    const int tiles_m = (g.M + BM - 1) / BM, per = group_m * tiles_n, first = (tile / per) * group_m;
+    const int gsz = min(tiles_m - first, group_m), r = tile % per;
+    mt = first + r % gsz, nt = r / gsz;
+  }
+  const int m0 = mt * BM, n0 = nt * BN;
 
   const bf16* __restrict__ A = reinterpret_cast<const bf16*>(g.A);
   const bf16* __restrict__ B = reinterpret_cast<const bf16*>(g.B);
@@ -374,8 +384,18 @@ static void launch_cfg(const GemmArgs& g, hipStream_t s, int splitk) {
     require(tn * tm <= kMaxTiles, "gemm: too many tiles for split-K");
     ws = w.p, cnt = w.cnt;
   }
+  // group_m ~ sqrt(tiles per XCD), so each XCD's tile block is about square
+  static const bool grouping = [] {
+    const char* e = std::getenv("CAPGEN_GEMM_GROUP");
+    return !(e && e[0] == '0');
+  }();
+  int group_m = 0;
+  if (grouping) {
+    const double per_xcd = (double)tn * tm / 8.0;
+    group_m = std::max(1, std::min(tm, (int)std::lround(std::sqrt(per_xcd))));
+  }
   gemm_bf16_kernel<TO, TA, TB, BM, BN, WM, WN, ST>
-      <<<nblk, 64 * WM * WN, 0, s>>>(g, tn, nblk, g_zero_page[dev], splitk, ws, cnt);
+      <<<nblk, 64 * WM * WN, 0, s>>>(g, tn, nblk, g_zero_page[dev], splitk, ws, cnt, group_m);
 }
 
 // split-K workspace bound for any variant (tiles up to 256x128)

@@ -66,6 +66,15 @@ elif __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "one":
     M, N, K, ta, tb, f32, v = map(int, sys.argv[2:9])
     _lib.check(lib.capgen_debug_gemm_variant(v))
     run(M, N, K, ta, tb, f32)
+elif __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "kscan":
+    # per-tile cost model: exactly 256 tiles (one per CU), time vs K -> slope (per 64-deep
+    # K step) and intercept (fixed per-tile overhead)
+    for (v, M, N) in [(6, 1024, 1024), (12, 1024, 1024), (3, 2048, 2048), (1, 2048, 2048), (16, 2048, 2048)]:
+        _lib.check(lib.capgen_debug_gemm_variant(v + 100))
+        for K in (64, 128, 256, 512, 1024, 2048, 4096):
+            us = run(M, N, K, 0, 0, 0, reps=20)
+        print(f"--- variant {v}", flush=True)
+    _lib.check(lib.capgen_debug_gemm_variant(0))
 elif __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "sk":
     # split-K study: eager launches (the split-K workspace is per stream), event timing
     shapes = [(512, 512, 2304, 1, 1, 1), (2048, 512, 2304, 1, 1, 1), (2304, 512, 2048, 0, 0, 0),
