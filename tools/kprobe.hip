@@ -1,0 +1,110 @@
+// Launch-overhead probe for MI355X: what does one dependent kernel boundary cost on this
+// stack (ROCm 7, eager vs hipGraph, one stream vs an event fork/join to a second stream)?
+// Build: hipcc -O3 --offload-arch=gfx950 tools/kprobe.hip -o tools/kprobe
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <functional>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                      \
+  do {                                                                             \
+    hipError_t e = (x);                                                            \
+    if (e != hipSuccess) {                                                         \
+      std::printf("%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e));         \
+      std::exit(1);                                                                \
+    }                                                                              \
+  } while (0)
+
+__global__ void tiny(float* p) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) p[0] += 1.f;
+}
+// streaming copy, 16 B per lane
+__global__ void copyk(const float4* __restrict__ a, float4* __restrict__ b, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) b[i] = a[i];
+}
+
+static float time_it(hipStream_t s, int reps, const std::function<void()>& f) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  f();
+  CK(hipStreamSynchronize(s));
+  CK(hipEventRecord(e0, s));
+  for (int r = 0; r < reps; ++r) f();
+  CK(hipEventRecord(e1, s));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms * 1e3f / reps;
+}
+
+int main() {
+  hipStream_t s, s2;
+  CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+  hipEvent_t ef, ej;
+  CK(hipEventCreateWithFlags(&ef, hipEventDisableTiming));
+  CK(hipEventCreateWithFlags(&ej, hipEventDisableTiming));
+  float* p;
+  CK(hipMalloc(&p, 1 << 20));
+  const size_t nbytes = 1216 * 512 * 2 * 2;  // ~2.5 MB (an LN-sized read+write)
+  float4 *a, *b;
+  CK(hipMalloc(&a, nbytes));
+  CK(hipMalloc(&b, nbytes));
+  CK(hipMemset(a, 0, nbytes));
+  const int K = 200;
+  auto chain = [&](int grid, bool fork) {
+    for (int i = 0; i < K; ++i) {
+      tiny<<<grid, 256, 0, s>>>(p);
+      if (fork) {
+        CK(hipEventRecord(ef, s));
+        CK(hipStreamWaitEvent(s2, ef, 0));
+        tiny<<<grid, 256, 0, s2>>>(p + 64);
+        CK(hipEventRecord(ej, s2));
+        CK(hipStreamWaitEvent(s, ej, 0));
+      }
+    }
+  };
+  auto copies = [&]() {
+    for (int i = 0; i < K; ++i) copyk<<<1024, 256, 0, s>>>(a, b, nbytes / 16);
+  };
+  std::printf("eager tiny 1 WG       : %.2f us/kernel\n", time_it(s, 3, [&] { chain(1, false); }) / K);
+  std::printf("eager tiny 1024 WG    : %.2f us/kernel\n", time_it(s, 3, [&] { chain(1024, false); }) / K);
+  std::printf("eager copy 2.5MB      : %.2f us/kernel\n", time_it(s, 3, copies) / K);
+  std::printf("eager fork/join pair  : %.2f us/iter (2 kernels + 2 events)\n",
+              time_it(s, 3, [&] { chain(1024, true); }) / K);
+  // graphs
+  auto graph_of = [&](const std::function<void()>& f) {
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    f();
+    CK(hipStreamEndCapture(s, &g));
+    CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    return ge;
+  };
+  hipGraphExec_t g1 = graph_of([&] { chain(1024, false); });
+  hipGraphExec_t g2 = graph_of(copies);
+  hipGraphExec_t g3 = graph_of([&] { chain(1024, true); });
+  std::printf("graph tiny 1024 WG    : %.2f us/kernel\n", time_it(s, 3, [&] { CK(hipGraphLaunch(g1, s)); }) / K);
+  std::printf("graph copy 2.5MB      : %.2f us/kernel\n", time_it(s, 3, [&] { CK(hipGraphLaunch(g2, s)); }) / K);
+  std::printf("graph fork/join pair  : %.2f us/iter\n", time_it(s, 3, [&] { CK(hipGraphLaunch(g3, s)); }) / K);
+  // host enqueue rate
+  {
+    auto t0 = std::chrono::high_resolution_clock::now();
+    chain(1024, false);
+    auto t1 = std::chrono::high_resolution_clock::now();
+    CK(hipStreamSynchronize(s));
+    std::printf("host enqueue          : %.2f us/kernel\n",
+                std::chrono::duration<double, std::micro>(t1 - t0).count() / K);
+    t0 = std::chrono::high_resolution_clock::now();
+    chain(1024, true);
+    t1 = std::chrono::high_resolution_clock::now();
+    CK(hipStreamSynchronize(s));
+    std::printf("host enqueue fork/join: %.2f us/iter\n", std::chrono::duration<double, std::micro>(t1 - t0).count() / K);
+  }
+  return 0;
+}

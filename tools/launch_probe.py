@@ -16,8 +16,7 @@ cfg = preset("C2", dtype="bf16", dropout=0.3)
 dev = torch.device("cuda", 0)
 eng = Engine(cfg, dev)
 eng.load_state_dict({k: torch.from_numpy(v) for k, v in reference_init_state_dict(cfg, seed=0).items()})
-if len(sys.argv) > 1 and sys.argv[1] == "eager":
-    eng.set_graph(False)
+eng.set_graph(len(sys.argv) > 1 and sys.argv[1] == "graph")
 f, p, c = synthetic_batch(B, N, cfg.encode_dim_features, cfg.encode_dim_positions, T, cfg.num_vocab, seed=1000)
 f, p, c = f.to(dev, torch.bfloat16).contiguous(), p.to(dev).contiguous(), c.to(dev).contiguous()
 loss = torch.zeros(1, device=dev)
