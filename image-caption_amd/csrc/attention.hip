@@ -311,6 +311,7 @@ static void allow_big_lds(K kernel) {
 }
 
 void attention_fwd(const AttnGeom& g, void* o, float* probs, DType t, hipStream_t s) {
+  if (skip_mask() & 2) return;
   check_geom(g);
   if (g.Lq == 1 && g.dk == 64 && g.drop.seed_ptr == nullptr && g.q_ld % 8 == 0 && g.k_ld % 8 == 0 &&
       ((g.q_bs | g.k_bs) % 8) == 0) {  // KV-cached decode step
@@ -336,6 +337,7 @@ void attention_fwd(const AttnGeom& g, void* o, float* probs, DType t, hipStream_
 
 void attention_bwd(const AttnGeom& g, const float* probs, const void* dout, void* dq, void* dk, void* dv, DType t,
                    hipStream_t s) {
+  if (skip_mask() & 8) return;
   check_geom(g);
   if (t == DType::BF16 && attention_mfma_ok(g))
     return attention_bwd_mfma(g, (const bf16*)dout, (bf16*)dq, (bf16*)dk, (bf16*)dv, s);

@@ -25,6 +25,11 @@ inline void require(bool ok, const std::string& what) {
   if (!ok) throw Error(what);
 }
 
+// Diagnostic only (CAPGEN_SKIP bitmask, never set in production): skip a kernel class to
+// measure its marginal cost on the step's critical path.  1 LN fwd, 2 attention fwd, 4 LN bwd,
+// 8 attention bwd, 16 GEMM f32-out (weight gradients + classifier), 32 Adam, 64 bf16 GEMMs.
+int skip_mask();
+
 // ---- scalar conversions -------------------------------------------------------------
 __device__ __forceinline__ float to_f(float x) { return x; }
 __device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
@@ -111,5 +116,21 @@ struct Drop {
   uint32_t thresh;
   float scale;  // 1/(1-p)
 };
+
+// Row mask applied to a LayerNorm output / its gradient: row m is zeroed when
+// ids[m] == pad (decoder non_pad_mask, model.py:483-486) or valid[m] == 0 (encoder
+// non_pad_mask with encode_mask, model.py:356-359).
+struct RowMask {
+  const int32_t* ids = nullptr;
+  int64_t ids_ld = 1;  // ids of row m at ids[m * ids_ld]
+  int pad_idx = 0;
+  const uint8_t* valid = nullptr;
+};
+
+__device__ __forceinline__ bool row_kept(const RowMask& rm, int m) {
+  if (rm.ids && rm.ids[(int64_t)m * rm.ids_ld] == rm.pad_idx) return false;
+  if (rm.valid && !rm.valid[m]) return false;
+  return true;
+}
 
 }  // namespace capgen

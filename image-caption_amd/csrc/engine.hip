@@ -14,6 +14,9 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -255,6 +258,12 @@ struct capgen_engine {
   // single-stream graph launches in 0.1 ms but loses the stream overlap (5.5 ms).
   bool graph_on = false;
   hipGraphExec_t gexec = nullptr;
+  // eager step mode: the forward alone as a linear graph (CAPGEN_FWD_GRAPH=0 disables)
+  bool fwd_graph_on = [] {
+    const char* e = std::getenv("CAPGEN_FWD_GRAPH");
+    return !(e && e[0] == '0');
+  }();
+  hipGraphExec_t fexec = nullptr;
   struct Key {
     const void *f, *p, *c;
     float* loss;
@@ -266,7 +275,7 @@ struct capgen_engine {
       return f == o.f && p == o.p && c == o.c && loss == o.loss && ft == o.ft && B == o.B && N == o.N && T == o.T &&
              drop == o.drop && idx == o.idx && nimg == o.nimg;
     }
-  } gkey{};
+  } gkey{}, fkey{};
   std::vector<std::array<int, 3>> tuned_shapes;
   bool tuned(int B, int N, int T) const {
     for (auto& t : tuned_shapes)
@@ -312,6 +321,25 @@ struct capgen_engine {
     ga.relu = relu;
     gemm(ga, act, tout, false, false, s);
   }
+  // C = X . W^T into ln.a, then y = LayerNorm(drop(C + bias) + res (+ pe)) (modules.py:86-90).
+  // (Fusing the LayerNorm into the GEMM -- a row-block finisher reloading the rows write-through
+  // -- was measured slower than this separate launch: DESIGN.md section 6.)
+  void linear_ln(const void* X, int64_t ldx, int64_t woff, int64_t ldw, int M, int N, int K, const LnFwd& ln,
+                 hipStream_t s) {
+    linear(X, ldx, woff, ldw, const_cast<void*>(ln.a), N, act, M, N, K, nullptr, 0, s);
+    layernorm_fwd(ln, act, s);
+  }
+  // a LayerNorm backward descriptor (striped accumulators); b_off < 0: no producing-Linear bias
+  LnBwd lnb_desc(int M, int d, const void* dy, const void* v, const float* mean, const float* rstd, int64_t lng,
+                 int64_t lnb, int64_t b_off, RowMask mask, Drop drop, void* d_res, void* d_a) const {
+    LnBwd lb;
+    lb.M = M, lb.d = d, lb.dy = dy, lb.v = v, lb.mean = mean, lb.rstd = rstd, lb.gamma = P(lng), lb.mask = mask;
+    lb.drop = drop, lb.d_res = d_res, lb.d_a = d_a, lb.dgamma = GS(lng), lb.dbeta = GS(lnb);
+    lb.dbias = b_off >= 0 ? GS(b_off) : nullptr;
+    striped(lb);
+    return lb;
+  }
+
   // dX[M,K] (+)= alpha * dY[M,N] . W[N,K]
   void linear_dx(const void* dY, int64_t ldy, int64_t woff, int64_t ldw, void* dX, int64_t ldx, int M, int N, int K,
                  int beta, const void* relu_aux, const float* alpha_ptr, hipStream_t s, float* colsum = nullptr) {
@@ -458,6 +486,10 @@ struct capgen_engine {
       (void)hipGraphExecDestroy(gexec);
       gexec = nullptr;
     }
+    if (fexec) {
+      (void)hipGraphExecDestroy(fexec);
+      fexec = nullptr;
+    }
   }
 
   // ------------------------------------------------------------------------------------
@@ -482,12 +514,11 @@ struct capgen_engine {
     }
 
     // ---- encoder (model.py:294-332) ----
-    linear(a.Aenc, L.Kp, L.enc_emb_W, L.Kp, a.tmp, d, act, Me, d, L.Kp, nullptr, 0, s);
     {
       LnFwd ln;
       ln.M = Me, ln.d = d, ln.a = a.tmp, ln.gamma = P(L.enc_lng), ln.beta = P(L.enc_lnb);
       ln.y = a.X[0], ln.v_save = a.ev0, ln.mean = a.em0, ln.rstd = a.er0;
-      layernorm_fwd(ln, act, s);
+      linear_ln(a.Aenc, L.Kp, L.enc_emb_W, L.Kp, Me, d, L.Kp, ln, s);
     }
     RowMask emask{};
     if (cfg.encode_mask) emask.valid = a.valid;
@@ -507,30 +538,27 @@ struct capgen_engine {
       g.temperature = std::sqrt((float)dke);
       g.drop = mk_drop(pa, site(0, l, 0), drop_on);
       attention_fwd(g, A.att, keep_probs(g) ? A.P : nullptr, act, s);
-      linear(A.att, d, w.Wo, d, a.tmp, d, act, Me, d, d, nullptr, 0, s);
       LnFwd l1;
       l1.M = Me, l1.d = d, l1.a = a.tmp, l1.drop = mk_drop(p, site(0, l, 1), drop_on), l1.res = a.X[l];
       l1.gamma = P(w.ln1g), l1.beta = P(w.ln1b), l1.y = A.Y, l1.v_save = A.v1, l1.mean = A.m1, l1.rstd = A.r1;
-      layernorm_fwd(l1, act, s);
+      linear_ln(A.att, d, w.Wo, d, Me, d, d, l1, s);
       linear(A.Y, d, w.W1, d, A.H, L.fe, act, Me, L.fe, d, P(w.b1), 1, s);
-      linear(A.H, L.fe, w.W2, L.fe, a.tmp, d, act, Me, d, L.fe, nullptr, 0, s);
       LnFwd l2;
       l2.M = Me, l2.d = d, l2.a = a.tmp, l2.a_bias = P(w.b2), l2.drop = mk_drop(p, site(0, l, 2), drop_on);
       l2.res = A.Y, l2.gamma = P(w.ln2g), l2.beta = P(w.ln2b), l2.mask = emask;
       l2.y = a.X[l + 1], l2.v_save = A.v2, l2.mean = A.m2, l2.rstd = A.r2;
-      layernorm_fwd(l2, act, s);
+      linear_ln(A.H, L.fe, w.W2, L.fe, Me, d, L.fe, l2, s);
     }
     // cross-attention K/V of every decoder block in one GEMM over the encoder output
     linear(a.X[L.Le], d, L.Wkv_all, d, a.KV, (int64_t)L.Ld * 2 * dd, act, Me, L.Ld * 2 * dd, d, nullptr, 0, s);
 
     // ---- decoder (model.py:419-459) ----
     embedding_gather(P(L.emb), a.ids, 1, Md, L.dwe, a.E, act, s);
-    linear(a.E, L.dwe, L.Wel, L.dwe, a.tmp, dd, act, Md, dd, L.dwe, nullptr, 0, s);
     {
       LnFwd ln;
       ln.M = Md, ln.d = dd, ln.a = a.tmp, ln.pe = pe, ln.pe_L = Lq, ln.gamma = P(L.dec_lng), ln.beta = P(L.dec_lnb);
       ln.y = a.D[0], ln.v_save = a.dv0, ln.mean = a.dm0, ln.rstd = a.dr0;
-      layernorm_fwd(ln, act, s);
+      linear_ln(a.E, L.dwe, L.Wel, L.dwe, Md, dd, L.dwe, ln, s);
     }
     RowMask dmask{};
     dmask.ids = a.ids, dmask.pad_idx = cfg.pad_idx;
@@ -550,11 +578,10 @@ struct capgen_engine {
       g.temperature = std::sqrt((float)dkd);
       g.drop = mk_drop(pa, site(1, l, 3), drop_on);
       attention_fwd(g, A.atts, keep_probs(g) ? A.Ps : nullptr, act, s);
-      linear(A.atts, dd, w.Wo_s, dd, a.tmp, dd, act, Md, dd, dd, nullptr, 0, s);
       LnFwd l1;
       l1.M = Md, l1.d = dd, l1.a = a.tmp, l1.drop = mk_drop(p, site(1, l, 4), drop_on), l1.res = a.D[l];
       l1.gamma = P(w.lsg), l1.beta = P(w.lsb), l1.y = A.D1, l1.v_save = A.vs, l1.mean = A.ms, l1.rstd = A.rs;
-      layernorm_fwd(l1, act, s);
+      linear_ln(A.atts, dd, w.Wo_s, dd, Md, dd, dd, l1, s);
       // cross attention over the encoder output, context mask = region key-pad (model.py:82)
       linear(A.D1, dd, w.Wq_c, dd, A.qc, dd, act, Md, dd, dd, nullptr, 0, s);
       AttnGeom c;
@@ -567,19 +594,17 @@ struct capgen_engine {
       c.temperature = std::sqrt((float)dkd);
       c.drop = mk_drop(pa, site(1, l, 5), drop_on);
       attention_fwd(c, A.attc, keep_probs(c) ? A.Pc : nullptr, act, s);
-      linear(A.attc, dd, w.Wo_c, dd, a.tmp, dd, act, Md, dd, dd, nullptr, 0, s);
       LnFwd l2;
       l2.M = Md, l2.d = dd, l2.a = a.tmp, l2.drop = mk_drop(p, site(1, l, 6), drop_on), l2.res = A.D1;
       l2.gamma = P(w.lcg), l2.beta = P(w.lcb), l2.y = A.D2, l2.v_save = A.vc, l2.mean = A.mc, l2.rstd = A.rc;
-      layernorm_fwd(l2, act, s);
+      linear_ln(A.attc, dd, w.Wo_c, dd, Md, dd, dd, l2, s);
       // FFN, then x non_pad (modules.py:201-204)
       linear(A.D2, dd, w.W1, dd, A.H, L.fd, act, Md, L.fd, dd, P(w.b1), 1, s);
-      linear(A.H, L.fd, w.W2, L.fd, a.tmp, dd, act, Md, dd, L.fd, nullptr, 0, s);
       LnFwd l3;
       l3.M = Md, l3.d = dd, l3.a = a.tmp, l3.a_bias = P(w.b2), l3.drop = mk_drop(p, site(1, l, 7), drop_on);
       l3.res = A.D2, l3.gamma = P(w.lfg), l3.beta = P(w.lfb), l3.mask = dmask;
       l3.y = a.D[l + 1], l3.v_save = A.vf, l3.mean = A.mf, l3.rstd = A.rf;
-      layernorm_fwd(l3, act, s);
+      linear_ln(A.H, L.fd, w.W2, L.fd, Md, dd, L.fd, l3, s);
     }
     // ---- classifier + CE (model.py:93-96) ----
     linear(a.D[L.Ld], dd, L.Wc, dd, a.logits, L.V, DType::F32, Md, L.V, dd, P(L.bc), 0, s);
@@ -598,40 +623,57 @@ struct capgen_engine {
     CAPGEN_HIP(hipStreamWaitEvent(to, e, 0));
   }
   void fork(hipStream_t s) { dep(s, es2, ev_fork); }
-  void join(hipStream_t s) { dep(es2, s, ev_join); }
+  void join(hipStream_t s) {
+    flush(s);
+    dep(es2, s, ev_join);
+  }
+  // Weight-gradient GEMMs are queued and issued on es2 in one batch per block (flush): an event
+  // record/wait pair costs the recording stream ~7 us of bubble on ROCm 7 (tools/kprobe.hip:
+  // 13 us per eager fork/join pair), so the critical stream records one event per block instead
+  // of one per weight.  Every buffer a queued dW reads is per block (or never rewritten in the
+  // backward pass), so issuing it later is hazard-free.
+  struct DwJob {
+    const void *dY, *X;
+    int64_t ldy, ldx, goff, ldg;
+    int M, N, K;
+    const float* alpha_ptr;
+  };
+  std::vector<DwJob> dw_pending;
   void dw_side(const void* dY, int64_t ldy, const void* X, int64_t ldx, int64_t goff, int64_t ldg, int M, int N,
                int K, const float* alpha_ptr, hipStream_t s) {
+    if (es2 == s) {
+      linear_dw(dY, ldy, X, ldx, goff, ldg, M, N, K, alpha_ptr, s);
+      return;
+    }
+    dw_pending.push_back(DwJob{dY, X, ldy, ldx, goff, ldg, M, N, K, alpha_ptr});
+  }
+  // es2 waits for everything issued on s so far, then runs the queued weight-gradient GEMMs
+  void flush(hipStream_t s) {
     fork(s);
-    linear_dw(dY, ldy, X, ldx, goff, ldg, M, N, K, alpha_ptr, es2);
+    for (const DwJob& j : dw_pending)
+      linear_dw(j.dY, j.ldy, j.X, j.ldx, j.goff, j.ldg, j.M, j.N, j.K, j.alpha_ptr, es2);
+    dw_pending.clear();
   }
 
   // one FFN + LayerNorm block backward; g_in = grad wrt block output, writes grad wrt the
   // block input (residual) to r_out.  X = block input, H = hidden activations.
-  void ffn_bwd(int M, int d, int f, const void* g_in, const void* X, const void* H, const void* v, const float* mean,
-               const float* rstd, int64_t W1, int64_t b1, int64_t W2, int64_t b2, int64_t lng, int64_t lnb,
-               RowMask mask, Drop drop, void* r_out, void* gA, void* gH, hipStream_t s) {
-    LnBwd lb;
-    lb.M = M, lb.d = d, lb.dy = g_in, lb.v = v, lb.mean = mean, lb.rstd = rstd, lb.gamma = P(lng), lb.mask = mask;
-    lb.drop = drop, lb.d_res = r_out, lb.d_a = gA, lb.dgamma = GS(lng), lb.dbeta = GS(lnb), lb.dbias = GS(b2);
-    striped(lb);
+  // lb = the block's LayerNorm backward (dy = grad wrt block output, d_res -> r_out, d_a -> gA);
+  // X = block input, H = hidden activations.
+  void ffn_bwd(int M, int d, int f, const LnBwd& lb, const void* X, const void* H, int64_t W1, int64_t b1, int64_t W2,
+               void* gH, hipStream_t s) {
     layernorm_bwd(lb, act, s);
+    void* gA = lb.d_a;
     dw_side(gA, d, H, f, W2, f, M, d, f, nullptr, s);
     linear_dx(gA, d, W2, f, gH, f, M, d, f, 0, H, nullptr, s, GS(b1));  // x relu'(H); db1 = colsum
     dw_side(gH, f, X, d, W1, d, M, f, d, nullptr, s);
-    linear_dx(gH, f, W1, d, r_out, d, M, f, d, 1, nullptr, nullptr, s);
+    linear_dx(gH, f, W1, d, lb.d_res, d, M, f, d, 1, nullptr, nullptr, s);
   }
-  // MHA output projection + LayerNorm backward: g_in = grad wrt LN output; writes grad wrt
-  // residual (query input) into r_out and grad wrt the attention output into gATT.
-  void mha_out_bwd(int M, int d, const void* g_in, const void* att, const void* v, const float* mean,
-                   const float* rstd, int64_t Wo, int64_t lng, int64_t lnb, Drop drop, void* r_out, void* gA,
-                   void* gATT, hipStream_t s) {
-    LnBwd lb;
-    lb.M = M, lb.d = d, lb.dy = g_in, lb.v = v, lb.mean = mean, lb.rstd = rstd, lb.gamma = P(lng);
-    lb.drop = drop, lb.d_res = r_out, lb.d_a = gA, lb.dgamma = GS(lng), lb.dbeta = GS(lnb);
-    striped(lb);
+  // MHA output projection + LayerNorm backward: lb as above (d_res = grad wrt the residual /
+  // query input); writes grad wrt the attention output into gATT.
+  void mha_out_bwd(int M, int d, const LnBwd& lb, const void* att, int64_t Wo, void* gATT, hipStream_t s) {
     layernorm_bwd(lb, act, s);
-    dw_side(gA, d, att, d, Wo, d, M, d, d, nullptr, s);
-    linear_dx(gA, d, Wo, d, gATT, d, M, d, d, 0, nullptr, nullptr, s);
+    dw_side(lb.d_a, d, att, d, Wo, d, M, d, d, nullptr, s);
+    linear_dx(lb.d_a, d, Wo, d, gATT, d, M, d, d, 0, nullptr, nullptr, s);
   }
 
   // Adam over arena ranges; ranges are 64-element aligned so the bf16 shadow slices line up
@@ -647,10 +689,12 @@ struct capgen_engine {
   // bucket stream ec waits for both compute streams, all-reduces the bucket's gradients
   // over RCCL (DP) and runs Adam on it, overlapped with the rest of the backward pass.
   // Buckets are issued in reverse layer order: 12-20 MB each at C2, one per block.
+  // sync: first flush (es2 waits for s, queued dW issued); sync=false when es2 already holds
+  // every producer of the bucket's gradients (consecutive buckets after one flush)
   bool bstep = false;
-  void bucket(int64_t off, int64_t n, hipStream_t s) {
+  void bucket(int64_t off, int64_t n, hipStream_t s, bool sync = true) {
+    if (sync) flush(s);
     if (!bstep) return;
-    dep(s, ec, ev_b1);
     dep(es2, ec, ev_b2);
     if (comm) NCCL_CHECK(ncclAllReduce(grads + off, grads + off, (size_t)n, ncclFloat, ncclSum, comm, ec));
     adam_range(off, n, ec);
@@ -671,15 +715,55 @@ struct capgen_engine {
     CAPGEN_HIP(hipMemsetAsync(gstripe, 0, (size_t)NSTRIPE * n_small * sizeof(float), s));
     if (bstep) adam_prepare(step, cfg.lr, cfg.beta1, cfg.beta2, adam_scal, s);
 
+    RowMask dmask{};
+    dmask.ids = a.ids, dmask.pad_idx = cfg.pad_idx;
+    RowMask emask{};
+    if (cfg.encode_mask) emask.valid = a.valid;
+    // the LayerNorm backward of every block (model.py:86-90, 114-120 restated backward)
+    auto dec_ffn_lb = [&](int l, const void* dy, void* dres) {
+      const auto& A = a.dec[l];
+      const auto& w = L.dec[l];
+      return lnb_desc(Md, dd, dy, A.vf, A.mf, A.rf, w.lfg, w.lfb, w.b2, dmask, mk_drop(p, site(1, l, 7), on), dres,
+                      a.gdec[l].gAf);
+    };
+    auto dec_cross_lb = [&](int l, const void* dy, void* dres) {
+      const auto& A = a.dec[l];
+      const auto& w = L.dec[l];
+      return lnb_desc(Md, dd, dy, A.vc, A.mc, A.rc, w.lcg, w.lcb, -1, RowMask{}, mk_drop(p, site(1, l, 6), on), dres,
+                      a.gdec[l].gA2);
+    };
+    auto dec_self_lb = [&](int l, const void* dy, void* dres) {
+      const auto& A = a.dec[l];
+      const auto& w = L.dec[l];
+      return lnb_desc(Md, dd, dy, A.vs, A.ms, A.rs, w.lsg, w.lsb, -1, RowMask{}, mk_drop(p, site(1, l, 4), on), dres,
+                      a.gdec[l].gA1);
+    };
+    auto dec_emb_lb = [&](const void* dy) {  // LN(E.Wel^T + PE) (model.py:432-436): no residual, no dropout
+      return lnb_desc(Md, dd, dy, a.dv0, a.dm0, a.dr0, L.dec_lng, L.dec_lnb, -1, RowMask{}, Drop{}, nullptr, a.gAd);
+    };
+    auto enc_ffn_lb = [&](int l, const void* dy, void* dres) {
+      const auto& A = a.enc[l];
+      const auto& w = L.enc[l];
+      return lnb_desc(Me, d, dy, A.v2, A.m2, A.r2, w.ln2g, w.ln2b, w.b2, emask, mk_drop(p, site(0, l, 2), on), dres,
+                      a.genc[l].gAf);
+    };
+    auto enc_mha_lb = [&](int l, const void* dy, void* dres) {
+      const auto& A = a.enc[l];
+      const auto& w = L.enc[l];
+      return lnb_desc(Me, d, dy, A.v1, A.m1, A.r1, w.ln1g, w.ln1b, -1, RowMask{}, mk_drop(p, site(0, l, 1), on), dres,
+                      a.genc[l].gA1);
+    };
+    auto enc_emb_lb = [&](const void* dy) {
+      return lnb_desc(Me, d, dy, a.ev0, a.em0, a.er0, L.enc_lng, L.enc_lnb, -1, RowMask{}, Drop{}, nullptr, a.gAe);
+    };
+
     // classifier: dlogits are unscaled (softmax - onehot); grad_scale folds 1/count (+focal)
     fork(s);
     column_sum(a.dlogits, Md, L.V, L.V, 1.f, a.grad_scale, GS(L.bc), act, es2, NSTRIPE, n_small);
     linear_dw(a.dlogits, L.V, a.D[L.Ld], dd, L.Wc, dd, Md, L.V, dd, a.grad_scale, es2);
     linear_dx(a.dlogits, L.V, L.Wc, dd, a.gOut, dd, Md, L.V, dd, 0, nullptr, a.grad_scale, s);
-    bucket(L.Wc, L.n_dense - L.Wc, s);
+    bucket(L.Wc, L.n_dense - L.Wc, s);  // after the dX GEMM above: it reads Wc
 
-    RowMask dmask{};
-    dmask.ids = a.ids, dmask.pad_idx = cfg.pad_idx;
     const int64_t kvld = (int64_t)L.Ld * 2 * dd;
     void* gO = a.gOut;
     void* gR = a.gRes;
@@ -687,10 +771,9 @@ struct capgen_engine {
       const auto& w = L.dec[l];
       auto& A = a.dec[l];
       auto& gb = a.gdec[l];
-      ffn_bwd(Md, dd, L.fd, gO, A.D2, A.H, A.vf, A.mf, A.rf, w.W1, w.b1, w.W2, w.b2, w.lfg, w.lfb, dmask,
-              mk_drop(p, site(1, l, 7), on), gR, gb.gAf, gb.gH, s);  // gR = grad wrt D2
-      mha_out_bwd(Md, dd, gR, A.attc, A.vc, A.mc, A.rc, w.Wo_c, w.lcg, w.lcb, mk_drop(p, site(1, l, 6), on), gO,
-                  gb.gA2, gb.gATT2, s);  // gO = grad wrt D1 (residual part)
+      const LnBwd lffn = dec_ffn_lb(l, gO, gR), lcross = dec_cross_lb(l, gR, gO), lself = dec_self_lb(l, gO, gR);
+      ffn_bwd(Md, dd, L.fd, lffn, A.D2, A.H, w.W1, w.b1, w.W2, gb.gH, s);  // gR = grad wrt D2
+      mha_out_bwd(Md, dd, lcross, A.attc, w.Wo_c, gb.gATT2, s);            // gO = grad wrt D1 (residual part)
       AttnGeom c;
       c.B = B, c.H = Hd, c.Lq = Lq, c.Lk = N, c.dk = dkd;
       c.q = A.qc, c.q_ld = dd, c.q_bs = (int64_t)Lq * dd;
@@ -704,8 +787,7 @@ struct capgen_engine {
                     act, s);
       dw_side(gb.gQc, dd, A.D1, dd, w.Wq_c, dd, Md, dd, dd, nullptr, s);
       linear_dx(gb.gQc, dd, w.Wq_c, dd, gO, dd, Md, dd, dd, 1, nullptr, nullptr, s);  // gO = grad wrt D1
-      mha_out_bwd(Md, dd, gO, A.atts, A.vs, A.ms, A.rs, w.Wo_s, w.lsg, w.lsb, mk_drop(p, site(1, l, 4), on), gR,
-                  gb.gA1, gb.gATT1, s);  // gR = grad wrt D_l (residual part)
+      mha_out_bwd(Md, dd, lself, A.atts, w.Wo_s, gb.gATT1, s);  // gR = grad wrt D_l (residual part)
       AttnGeom g;
       g.B = B, g.H = Hd, g.Lq = Lq, g.Lk = Lq, g.dk = dkd;
       g.q = A.qkv, g.q_ld = 3 * dd, g.q_bs = (int64_t)Lq * 3 * dd;
@@ -726,11 +808,8 @@ struct capgen_engine {
     void* eO = gO == a.gOut ? a.gRes : a.gOut;  // the buffer gO is not using
     // decoder embedding: LN(E.Wel^T + PE) (model.py:432-436) -- off the critical path
     {
-      LnBwd lb;
-      lb.M = Md, lb.d = dd, lb.dy = gO, lb.v = a.dv0, lb.mean = a.dm0, lb.rstd = a.dr0, lb.gamma = P(L.dec_lng);
-      lb.d_a = a.gAd, lb.dgamma = GS(L.dec_lng), lb.dbeta = GS(L.dec_lnb);
-      striped(lb);
-      fork(s);
+      const LnBwd lb = dec_emb_lb(gO);
+      flush(s);  // issues the queued cross-K/V weight gradient first
       layernorm_bwd(lb, act, es2);
       linear_dw(a.gAd, dd, a.E, L.dwe, L.Wel, L.dwe, Md, dd, L.dwe, nullptr, es2);
       linear_dx(a.gAd, dd, L.Wel, L.dwe, a.gE, L.dwe, Md, dd, L.dwe, 0, nullptr, nullptr, es2);
@@ -744,20 +823,19 @@ struct capgen_engine {
     gR = a.tmp;
     linear_dx(a.gKV, kvld, L.Wkv_all, d, gO, d, Me, L.Ld * 2 * dd, d, 0, nullptr, nullptr, s);
     // the decoder-embedding branch (es2) has been issued: every decoder-side gradient is final
+    // the flush of the first bucket follows the dX GEMM above (it reads Wkv_all); es2 then holds
+    // every producer of the other three buckets
     bucket(L.Wkv_all, L.Wc - L.Wkv_all, s);               // cross K/V of all decoder blocks
-    bucket(L.Wel, L.dec[0].Wqkv - L.Wel, s);              // word-embedding projection
-    bucket(L.emb, L.enc_lng - L.emb, s);                  // word embedding table
-    bucket(L.dec_lng, L.total - L.dec_lng, s);            // decoder LN / biases, classifier bias
-    RowMask emask{};
-    if (cfg.encode_mask) emask.valid = a.valid;
+    bucket(L.Wel, L.dec[0].Wqkv - L.Wel, s, false);       // word-embedding projection
+    bucket(L.emb, L.enc_lng - L.emb, s, false);           // word embedding table
+    bucket(L.dec_lng, L.total - L.dec_lng, s, false);     // decoder LN / biases, classifier bias
     for (int l = L.Le - 1; l >= 0; --l) {
       const auto& w = L.enc[l];
       auto& A = a.enc[l];
       auto& gb = a.genc[l];
-      ffn_bwd(Me, d, L.fe, gO, A.Y, A.H, A.v2, A.m2, A.r2, w.W1, w.b1, w.W2, w.b2, w.ln2g, w.ln2b, emask,
-              mk_drop(p, site(0, l, 2), on), gR, gb.gAf, gb.gH, s);  // gR = grad wrt Y
-      mha_out_bwd(Me, d, gR, A.att, A.v1, A.m1, A.r1, w.Wo, w.ln1g, w.ln1b, mk_drop(p, site(0, l, 1), on), gO,
-                  gb.gA1, gb.gATT1, s);
+      const LnBwd lffn = enc_ffn_lb(l, gO, gR), lmha = enc_mha_lb(l, gR, gO);
+      ffn_bwd(Me, d, L.fe, lffn, A.Y, A.H, w.W1, w.b1, w.W2, gb.gH, s);  // gR = grad wrt Y
+      mha_out_bwd(Me, d, lmha, A.att, w.Wo, gb.gATT1, s);
       AttnGeom g;
       g.B = B, g.H = He, g.Lq = N, g.Lk = N, g.dk = dke;
       g.q = A.qkv, g.q_ld = 3 * d, g.q_bs = (int64_t)N * 3 * d;
@@ -773,18 +851,14 @@ struct capgen_engine {
       bucket(w.Wqkv, enc_end(l) - w.Wqkv, s);
     }
     {
-      LnBwd lb;
-      lb.M = Me, lb.d = d, lb.dy = gO, lb.v = a.ev0, lb.mean = a.em0, lb.rstd = a.er0, lb.gamma = P(L.enc_lng);
-      lb.d_a = a.gAe, lb.dgamma = GS(L.enc_lng), lb.dbeta = GS(L.enc_lnb);
-      striped(lb);
-      layernorm_bwd(lb, act, s);
+      layernorm_bwd(enc_emb_lb(gO), act, s);
       dw_side(a.gAe, d, a.Aenc, L.Kp, L.enc_emb_W, L.Kp, Me, d, L.Kp, nullptr, s);
     }
     join(s);
     stripe_reduce(GS(L.enc_lng), NSTRIPE, n_small, L.dec_lng - L.enc_lng, G(L.enc_lng), 0, s);
     if (bstep) {
       bucket(0, L.enc[0].Wqkv, s);                        // feature/position embedding
-      bucket(L.enc_lng, L.dec_lng - L.enc_lng, s);        // encoder LN / biases
+      bucket(L.enc_lng, L.dec_lng - L.enc_lng, s, false);  // encoder LN / biases
       dep(ec, s, ev_cj);
       bstep = false;
     }
@@ -822,10 +896,53 @@ struct capgen_engine {
     enter(cs);
     Key k{f, pos, caps, loss, (int)ft, B, N, T, training, in_idx, in_n_img};
     auto body = [&]() {
+      static const bool host_timing = std::getenv("CAPGEN_HOST_TIMING") != nullptr;  // diagnostic
+      static double tf = 0, tb = 0;
+      static int nsteps = 0;
+      auto t0 = std::chrono::steady_clock::now();
       forward(f, ft, pos, caps, B, N, T, loss, training, es);
+      auto t1 = std::chrono::steady_clock::now();
       backward(es, /*step_params=*/true);  // + bucketed RCCL all-reduce (DP) and Adam
+      if (host_timing) {
+        auto t2 = std::chrono::steady_clock::now();
+        tf += std::chrono::duration<double, std::micro>(t1 - t0).count();
+        tb += std::chrono::duration<double, std::micro>(t2 - t1).count();
+        if (++nsteps % 20 == 0) {
+          std::fprintf(stderr, "[capgen host] enqueue per step: forward %.1f us, backward %.1f us\n", tf / 20, tb / 20);
+          tf = tb = 0;
+        }
+      }
     };
-    if (!graph_on) {
+    if (!graph_on && fwd_graph_on && !comm) {
+      // forward replayed as one linear hipGraph (cheap to launch: ~0.1 us/node of host time vs
+      // ~2.7 us per eager launch, tools/kprobe.hip); backward issued eagerly on three streams
+      // (a multi-branch graph costs the same host time per node as eager issue on ROCm 7)
+      if (!(fexec && fkey == k)) {
+        drop_graph();
+        if (!tuned(B, N, T)) {  // autotune every GEMM shape outside the capture
+          forward(f, ft, pos, caps, B, N, T, loss, /*drop_on=*/false, es);
+          backward(es);
+          CAPGEN_HIP(hipStreamSynchronize(es));
+          tuned_shapes.push_back({B, N, T});
+        }
+        hipGraph_t graph = nullptr;
+        CAPGEN_HIP(hipStreamBeginCapture(es, hipStreamCaptureModeThreadLocal));
+        try {
+          forward(f, ft, pos, caps, B, N, T, loss, training, es);
+        } catch (...) {
+          (void)hipStreamEndCapture(es, &graph);
+          if (graph) (void)hipGraphDestroy(graph);
+          throw;
+        }
+        CAPGEN_HIP(hipStreamEndCapture(es, &graph));
+        CAPGEN_HIP(hipGraphInstantiate(&fexec, graph, nullptr, nullptr, 0));
+        CAPGEN_HIP(hipGraphDestroy(graph));
+        fkey = k;
+      }
+      CAPGEN_HIP(hipGraphLaunch(fexec, es));
+      fB = B, fN = N, fT = T, fwd_drop = training;  // host state forward() would have set
+      backward(es, /*step_params=*/true);
+    } else if (!graph_on) {
       body();
     } else {
       if (!(gexec && gkey == k)) {
@@ -1187,6 +1304,8 @@ int capgen_create(const capgen_config* cfg, int device, capgen_t** out) {
     h->device = device;
     h->act = dt(cfg->dtype);
     const size_t n = (size_t)h->L.total;
+    // (stream priorities measured: no gain for one engine, and with two engines in a process
+    // the high-priority queues serialised each other -- plain streams)
     CAPGEN_HIP(hipStreamCreateWithFlags(&h->es, hipStreamNonBlocking));
     // CAPGEN_STREAMS (experiment knob): 3 = critical path + weight-grad + bucket streams
     // (default), 2 = buckets on the weight-grad stream, 1 = everything on one stream

@@ -212,6 +212,8 @@ static void launch_layout(const GemmArgs& g, bool ta, bool tb, hipStream_t s) {
 
 void gemm(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0) return;
+  if ((skip_mask() & 16) && out == DType::F32) return;
+  if ((skip_mask() & 64) && out == DType::BF16) return;
   const int vec = in == DType::F32 ? 4 : 8;
   // the contiguous dimension of each operand is read in 16-B vectors
   require((ta ? g.M : g.K) % vec == 0 && g.lda % vec == 0, "gemm: A contiguous dim/ld not a multiple of 16 B");

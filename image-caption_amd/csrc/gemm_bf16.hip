@@ -58,7 +58,9 @@ void* g_zero_page[64] = {};
 __device__ __forceinline__ int swz_k(int row, int chunk) { return chunk ^ (((row >> 1) ^ (row >> 4)) & 7); }
 template <int ROWS>
 __device__ __forceinline__ int swz_t(int k, int chunk) {                                   // [k][ROWS]
-  return ROWS == 128 ? chunk ^ ((k & 7) << 1) : chunk ^ (((k >> 1) & 3) << 1);
+  if constexpr (ROWS == 128) return chunk ^ ((k & 7) << 1);
+  else if constexpr (ROWS == 64) return chunk ^ (((k >> 1) & 3) << 1);
+  else return chunk ^ (((k >> 2) & 1) << 1);  // 32 rows = 4 chunks per K row
 }
 
 template <bool TRANS, int ROWS, int NW>
@@ -408,12 +410,13 @@ int g_variant = 0;  // experiment selector (capgen_debug_gemm_variant); 0 = tune
 // Tile / wave-grid / pipeline-depth variants.  Every variant accumulates the same K tiles
 // in the same order with the same MFMA sequence, so results are bit-identical across
 // variants: the choice is a pure speed decision (made per shape by the autotuner).
-constexpr int NVARIANTS = 16;
+constexpr int NVARIANTS = 22;
 const char* kVariantName[NVARIANTS + 1] = {"auto",        "128x128w4s3", "128x128w8s2",  "128x128w4s2",
                                            "128x64w4s2",  "64x128w4s2",  "64x64w4s2",    "64x64w4s3",
                                            "128x64w8s2",  "256x128w16s2", "128x128w16s2", "256x64w8s2",
                                            "64x64w4s4",   "64x64w4s6",   "128x64w4s4",   "64x128w4s4",
-                                           "128x128w4s4"};
+                                           "128x128w4s4", "32x64w4s2",   "64x32w4s2",    "32x32w4s2",
+                                           "64x64w8s2",   "32x64w4s3",   "64x32w4s3"};
 
 template <typename TO, bool TA, bool TB>
 static void launch_variant(int v, const GemmArgs& g, hipStream_t s, int sk = 1) {
@@ -434,6 +437,13 @@ static void launch_variant(int v, const GemmArgs& g, hipStream_t s, int sk = 1) 
     case 14: return launch_cfg<TO, TA, TB, 128, 64, 2, 2, 4>(g, s, sk);
     case 15: return launch_cfg<TO, TA, TB, 64, 128, 2, 2, 4>(g, s, sk);
     case 16: return launch_cfg<TO, TA, TB, 128, 128, 2, 2, 4>(g, s, sk);
+    // small tiles: more workgroups per CU for the latency-bound small GEMMs of the step
+    case 17: return launch_cfg<TO, TA, TB, 32, 64, 2, 2, 2>(g, s, sk);
+    case 18: return launch_cfg<TO, TA, TB, 64, 32, 2, 2, 2>(g, s, sk);
+    case 19: return launch_cfg<TO, TA, TB, 32, 32, 2, 2, 2>(g, s, sk);
+    case 20: return launch_cfg<TO, TA, TB, 64, 64, 4, 2, 2>(g, s, sk);
+    case 21: return launch_cfg<TO, TA, TB, 32, 64, 2, 2, 3>(g, s, sk);
+    case 22: return launch_cfg<TO, TA, TB, 64, 32, 2, 2, 3>(g, s, sk);
     default: throw Error("gemm: unknown variant");
   }
 }

@@ -5,16 +5,6 @@
 
 namespace capgen {
 
-// Row mask applied to a LayerNorm output / its gradient: row m is zeroed when
-// ids[m] == pad (decoder non_pad_mask, model.py:483-486) or valid[m] == 0 (encoder
-// non_pad_mask with encode_mask, model.py:356-359).
-struct RowMask {
-  const int32_t* ids = nullptr;
-  int64_t ids_ld = 1;  // ids of row m at ids[m * ids_ld]
-  int pad_idx = 0;
-  const uint8_t* valid = nullptr;
-};
-
 // y = LN(drop(a + a_bias) + res + pe[m % pe_L]) * rowmask          (modules.py:86-90, 114-120)
 struct LnFwd {
   int M = 0, d = 0;

@@ -6,19 +6,31 @@
 // workgroup and issues one f32 atomic per column per workgroup.
 // CE: one workgroup per row (V=10000 f32 logits stay in L2 for the 3 passes).
 // Adam: 16-B vectorised streaming over the flat parameter arena (HBM bound).
+#include <cstdlib>
+
 #include "ops.h"
 
 namespace capgen {
 
+int skip_mask() {
+  static const int m = [] {
+    const char* e = std::getenv("CAPGEN_SKIP");
+    return e ? std::atoi(e) : 0;
+  }();
+  return m;
+}
+
 constexpr int LN_THREADS = 256;  // 4 rows per workgroup
 constexpr float LN_EPS = 1e-6f;  // modules.py:57,105
 
-__device__ __forceinline__ bool row_kept(const RowMask& rm, int m) {
-  if (rm.ids && rm.ids[(int64_t)m * rm.ids_ld] == rm.pad_idx) return false;
-  if (rm.valid && !rm.valid[m]) return false;
-  return true;
-}
 
+// Every global load of the row (input, residual, bias, positional row, gamma, beta, row mask,
+// dropout seed) is issued before the first store: the kernel pays ONE memory round trip (the
+// stores could alias the parameter pointers, so the compiler would not hoist them itself).
+template <int DPL>
+__device__ __forceinline__ void load_f32(const float* p, float (&out)[DPL]) {
+  load_f<float, DPL>(p, out);
+}
 template <typename T, int DPL>
 __global__ void __launch_bounds__(LN_THREADS) ln_fwd_kernel(LnFwd a) {
   const int lane = threadIdx.x & 63;
@@ -26,30 +38,32 @@ __global__ void __launch_bounds__(LN_THREADS) ln_fwd_kernel(LnFwd a) {
   if (m >= a.M) return;
   const int d = a.d, c0 = lane * DPL;
   const int64_t base = (int64_t)m * d + c0;
-  float x[DPL];
+  float x[DPL], r[DPL], bias[DPL], pe[DPL], gm[DPL], bt[DPL];
   load_f<T, DPL>(reinterpret_cast<const T*>(a.a) + base, x);
+  if (a.res) load_f<T, DPL>(reinterpret_cast<const T*>(a.res) + base, r);
+  if (a.a_bias) load_f32<DPL>(a.a_bias + c0, bias);
+  if (a.pe) load_f32<DPL>(a.pe + (int64_t)(m % a.pe_L) * d + c0, pe);
+  load_f32<DPL>(a.gamma + c0, gm);
+  load_f32<DPL>(a.beta + c0, bt);
+  const bool kept = row_kept(a.mask, m);
+  const uint64_t seed = a.drop.seed_ptr ? *a.drop.seed_ptr : 0;
   if (a.a_bias) {
 #pragma unroll
-    for (int e = 0; e < DPL; ++e) x[e] += a.a_bias[c0 + e];
+    for (int e = 0; e < DPL; ++e) x[e] += bias[e];
   }
   if (a.drop.seed_ptr) {
-    const uint64_t seed = *a.drop.seed_ptr;
 #pragma unroll
     for (int e = 0; e < DPL; ++e)
       x[e] = drop_keep(seed, a.drop.site, (uint32_t)(base + e), a.drop.thresh) ? x[e] * a.drop.scale : 0.f;
   }
   if (a.res) {
-    float r[DPL];
-    load_f<T, DPL>(reinterpret_cast<const T*>(a.res) + base, r);
 #pragma unroll
     for (int e = 0; e < DPL; ++e) x[e] += r[e];
   }
   if (a.pe) {
-    const float* pe = a.pe + (int64_t)(m % a.pe_L) * d + c0;
 #pragma unroll
     for (int e = 0; e < DPL; ++e) x[e] += pe[e];
   }
-  if (a.v_save) store_f<T, DPL>(reinterpret_cast<T*>(a.v_save) + base, x);
   float s = 0.f;
 #pragma unroll
   for (int e = 0; e < DPL; ++e) s += x[e];
@@ -62,10 +76,11 @@ __global__ void __launch_bounds__(LN_THREADS) ln_fwd_kernel(LnFwd a) {
   }
   const float var = wave_sum(q) / (float)d;
   const float rstd = 1.0f / sqrtf(var + LN_EPS);
-  const float keep = row_kept(a.mask, m) ? 1.f : 0.f;
+  const float keep = kept ? 1.f : 0.f;
   float y[DPL];
 #pragma unroll
-  for (int e = 0; e < DPL; ++e) y[e] = ((x[e] - mean) * rstd * a.gamma[c0 + e] + a.beta[c0 + e]) * keep;
+  for (int e = 0; e < DPL; ++e) y[e] = ((x[e] - mean) * rstd * gm[e] + bt[e]) * keep;
+  if (a.v_save) store_f<T, DPL>(reinterpret_cast<T*>(a.v_save) + base, x);
   store_f<T, DPL>(reinterpret_cast<T*>(a.y) + base, y);
   if (lane == 0) {
     if (a.mean) a.mean[m] = mean;
@@ -80,15 +95,16 @@ __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(LnBwd a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int d = a.d, c0 = lane * DPL;
   float dg[DPL], db[DPL], dz[DPL], gm[DPL];
+  load_f<float, DPL>(a.gamma + c0, gm);
 #pragma unroll
-  for (int e = 0; e < DPL; ++e) dg[e] = db[e] = dz[e] = 0.f, gm[e] = a.gamma[c0 + e];
+  for (int e = 0; e < DPL; ++e) dg[e] = db[e] = dz[e] = 0.f;
   const uint64_t seed = a.drop.seed_ptr ? *a.drop.seed_ptr : 0;
   const int stride = gridDim.x * (LN_THREADS / 64);
   for (int m0 = blockIdx.x * (LN_THREADS / 64) + wave; m0 < a.M; m0 += R * stride) {
     float dy[R][DPL], v[R][DPL], mean[R], rstd[R];
-    bool on[R];
+    bool on[R], kept[R];
 #pragma unroll
-    for (int u = 0; u < R; ++u) {
+    for (int u = 0; u < R; ++u) {  // every load of both rows (row mask included) first
       const int m = m0 + u * stride;
       on[u] = m < a.M;
       if (on[u]) {
@@ -96,6 +112,7 @@ __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(LnBwd a) {
         load_f<T, DPL>(reinterpret_cast<const T*>(a.dy) + base, dy[u]);
         load_f<T, DPL>(reinterpret_cast<const T*>(a.v) + base, v[u]);
         mean[u] = a.mean[m], rstd[u] = a.rstd[m];
+        kept[u] = row_kept(a.mask, m);
       }
     }
 #pragma unroll
@@ -103,7 +120,7 @@ __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(LnBwd a) {
       if (!on[u]) continue;
       const int m = m0 + u * stride;
       const int64_t base = (int64_t)m * d + c0;
-      const float keep = row_kept(a.mask, m) ? 1.f : 0.f;
+      const float keep = kept[u] ? 1.f : 0.f;
       float g[DPL], xh[DPL], s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int e = 0; e < DPL; ++e) {
@@ -170,7 +187,7 @@ static void ln_fwd_dispatch(const LnFwd& a, hipStream_t s) {
   }
 }
 void layernorm_fwd(const LnFwd& a, DType t, hipStream_t s) {
-  if (a.M <= 0) return;
+  if (a.M <= 0 || (skip_mask() & 1)) return;
   if (t == DType::F32) ln_fwd_dispatch<float>(a, s);
   else ln_fwd_dispatch<bf16>(a, s);
   CAPGEN_HIP(hipGetLastError());
@@ -190,7 +207,7 @@ static void ln_bwd_dispatch(const LnBwd& a, hipStream_t s) {
   }
 }
 void layernorm_bwd(const LnBwd& a, DType t, hipStream_t s) {
-  if (a.M <= 0) return;
+  if (a.M <= 0 || (skip_mask() & 4)) return;
   if (t == DType::F32) ln_bwd_dispatch<float>(a, s);
   else ln_bwd_dispatch<bf16>(a, s);
   CAPGEN_HIP(hipGetLastError());
@@ -518,6 +535,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float4* __restrict__ p, const
 void adam_update(float* p, const float* g, float* m, float* v, size_t n, float b1, float b2, float eps,
                  const float* scal, bf16* shadow, size_t n_shadow, hipStream_t s) {
   require(n % 4 == 0 && n_shadow % 4 == 0, "adam: arena size must be a multiple of 4");
+  if (skip_mask() & 32) return;
   size_t n4 = n / 4;
   int grid = (int)std::min<size_t>((n4 + 255) / 256, 256 * 8);
   adam_kernel<<<grid, 256, 0, s>>>((float4*)p, (const float4*)g, (float4*)m, (float4*)v, n4, b1, b2, eps, scal,

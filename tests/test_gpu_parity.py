@@ -277,7 +277,7 @@ def test_gemm_kernel_vs_torch(in_dt, ta, tb, M, N, K):
     assert (Cd.cpu() - ref).abs().max().item() <= tol
 
 
-@pytest.mark.parametrize("variant", list(range(1, 17)) + [206, 303, 403, 612, 813, 1314])
+@pytest.mark.parametrize("variant", list(range(1, 23)) + [206, 303, 403, 612, 813, 1314, 217, 319, 420])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 1)])
 def test_gemm_every_variant_and_splitk(variant, ta, tb):
     """Each tile/wave/stage variant (and split-K factor: variant + 100*splitk) computes the

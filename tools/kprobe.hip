@@ -92,6 +92,38 @@ int main() {
   std::printf("graph tiny 1024 WG    : %.2f us/kernel\n", time_it(s, 3, [&] { CK(hipGraphLaunch(g1, s)); }) / K);
   std::printf("graph copy 2.5MB      : %.2f us/kernel\n", time_it(s, 3, [&] { CK(hipGraphLaunch(g2, s)); }) / K);
   std::printf("graph fork/join pair  : %.2f us/iter\n", time_it(s, 3, [&] { CK(hipGraphLaunch(g3, s)); }) / K);
+  // two independent chains in ONE graph (fork at the start, join at the end): is a 2-branch
+  // graph launched as cheaply as a linear one?
+  {
+    auto two = [&]() {
+      CK(hipEventRecord(ef, s));
+      CK(hipStreamWaitEvent(s2, ef, 0));
+      for (int i = 0; i < K; ++i) {
+        tiny<<<1024, 256, 0, s>>>(p);
+        tiny<<<1024, 256, 0, s2>>>(p + 64);
+      }
+      CK(hipEventRecord(ej, s2));
+      CK(hipStreamWaitEvent(s, ej, 0));
+    };
+    hipGraphExec_t g4 = graph_of(two);
+    std::printf("graph 2 chains        : %.2f us/kernel-pair\n", time_it(s, 3, [&] { CK(hipGraphLaunch(g4, s)); }) / K);
+    CK(hipStreamSynchronize(s));
+    auto t0 = std::chrono::high_resolution_clock::now();
+    CK(hipGraphLaunch(g4, s));
+    auto t1 = std::chrono::high_resolution_clock::now();
+    CK(hipStreamSynchronize(s));
+    std::printf("host graph 2 chains   : %.2f us/kernel-pair\n", std::chrono::duration<double, std::micro>(t1 - t0).count() / K);
+    t0 = std::chrono::high_resolution_clock::now();
+    CK(hipGraphLaunch(g1, s));
+    t1 = std::chrono::high_resolution_clock::now();
+    CK(hipStreamSynchronize(s));
+    std::printf("host graph 1 chain    : %.2f us/kernel\n", std::chrono::duration<double, std::micro>(t1 - t0).count() / K);
+    t0 = std::chrono::high_resolution_clock::now();
+    two();
+    t1 = std::chrono::high_resolution_clock::now();
+    CK(hipStreamSynchronize(s));
+    std::printf("host eager 2 chains   : %.2f us/kernel-pair\n", std::chrono::duration<double, std::micro>(t1 - t0).count() / K);
+  }
   // host enqueue rate
   {
     auto t0 = std::chrono::high_resolution_clock::now();
@@ -106,5 +138,27 @@ int main() {
     CK(hipStreamSynchronize(s));
     std::printf("host enqueue fork/join: %.2f us/iter\n", std::chrono::duration<double, std::micro>(t1 - t0).count() / K);
   }
+  // host price of the runtime calls a launch wrapper tends to make
+  auto host_us = [&](const char* what, const std::function<void()>& f) {
+    const int R = 2000;
+    f();
+    auto t0 = std::chrono::high_resolution_clock::now();
+    for (int i = 0; i < R; ++i) f();
+    auto t1 = std::chrono::high_resolution_clock::now();
+    std::printf("host %-22s: %.3f us/call\n", what, std::chrono::duration<double, std::micro>(t1 - t0).count() / R);
+  };
+  int dev;
+  hipStreamCaptureStatus cst;
+  host_us("hipGetDevice", [&] { (void)hipGetDevice(&dev); });
+  host_us("hipGetLastError", [&] { (void)hipGetLastError(); });
+  host_us("hipStreamIsCapturing", [&] { (void)hipStreamIsCapturing(s, &cst); });
+  host_us("hipSetDevice", [&] { (void)hipSetDevice(0); });
+  CK(hipStreamSynchronize(s));
+  host_us("launch tiny (1 WG)", [&] { tiny<<<1, 64, 0, s>>>(p); });
+  CK(hipStreamSynchronize(s));
+  host_us("hipEventRecord", [&] { (void)hipEventRecord(ef, s); });
+  CK(hipStreamSynchronize(s));
+  host_us("hipStreamWaitEvent", [&] { (void)hipStreamWaitEvent(s2, ef, 0); });
+  CK(hipDeviceSynchronize());
   return 0;
 }
