@@ -117,6 +117,16 @@ struct Drop {
   float scale;  // 1/(1-p)
 };
 
+// one torch.optim.Adam element update (torch 2.x single-tensor path, no weight decay):
+// neg_step = -lr / (1 - b1^t), bc2s = sqrt(1 - b2^t); b1c = 1 - b1, b2c = 1 - b2
+__device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, float b1c, float b2, float b2c,
+                                         float eps, float neg_step, float bc2s) {
+  m = m + b1c * (g - m);                      // exp_avg.lerp_(grad, 1 - beta1)
+  v = v * b2 + b2c * (g * g);                 // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
+  const float denom = sqrtf(v) / bc2s + eps;  // (exp_avg_sq.sqrt() / bc2_sqrt).add_(eps)
+  p = p + (neg_step * m) / denom;             // param.addcdiv_(exp_avg, denom, value=-step_size)
+}
+
 // Row mask applied to a LayerNorm output / its gradient: row m is zeroed when
 // ids[m] == pad (decoder non_pad_mask, model.py:483-486) or valid[m] == 0 (encoder
 // non_pad_mask with encode_mask, model.py:356-359).

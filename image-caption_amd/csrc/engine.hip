@@ -639,6 +639,10 @@ struct capgen_engine {
     const float* alpha_ptr;
   };
   std::vector<DwJob> dw_pending;
+  bool group_dw = [] {  // CAPGEN_GROUP_DW=0: one launch per weight (A/B experiments, tests)
+    const char* e = std::getenv("CAPGEN_GROUP_DW");
+    return !(e && e[0] == '0');
+  }();
   void dw_side(const void* dY, int64_t ldy, const void* X, int64_t ldx, int64_t goff, int64_t ldg, int M, int N,
                int K, const float* alpha_ptr, hipStream_t s) {
     if (es2 == s) {
@@ -647,16 +651,34 @@ struct capgen_engine {
     }
     dw_pending.push_back(DwJob{dY, X, ldy, ldx, goff, ldg, M, N, K, alpha_ptr});
   }
+  GemmArgs dw_args(const DwJob& j) const {
+    GemmArgs ga;
+    ga.M = j.N, ga.N = j.K, ga.K = j.M, ga.A = j.dY, ga.lda = j.ldy, ga.B = j.X, ga.ldb = j.ldx;
+    ga.C = G(j.goff), ga.ldc = j.ldg, ga.alpha_ptr = j.alpha_ptr;
+    return ga;
+  }
+  // run weight-gradient jobs on stream st now: in bf16 mode as grouped launches (every dW tile
+  // of a block in one grid: better chip fill than 4-6 small launches, tools/dw_variant_probe.sh)
+  void dw_launch(const DwJob* jobs, size_t n, hipStream_t st) {
+    if (act == DType::BF16 && group_dw) {
+      std::vector<GemmArgs> probs;
+      for (size_t i = 0; i < n; ++i) probs.push_back(dw_args(jobs[i]));
+      for (size_t i = 0; i < n; i += kMaxGroup)
+        gemm_grouped(probs.data() + i, (int)std::min<size_t>(kMaxGroup, n - i), DType::F32, true, true, st);
+    } else {
+      for (size_t i = 0; i < n; ++i) {
+        const DwJob& j = jobs[i];
+        linear_dw(j.dY, j.ldy, j.X, j.ldx, j.goff, j.ldg, j.M, j.N, j.K, j.alpha_ptr, st);
+      }
+    }
+  }
   // es2 waits for everything issued on s so far, then runs the queued weight-gradient GEMMs
   void flush(hipStream_t s) {
     fork(s);
-    for (const DwJob& j : dw_pending)
-      linear_dw(j.dY, j.ldy, j.X, j.ldx, j.goff, j.ldg, j.M, j.N, j.K, j.alpha_ptr, es2);
+    dw_launch(dw_pending.data(), dw_pending.size(), es2);
     dw_pending.clear();
   }
 
-  // one FFN + LayerNorm block backward; g_in = grad wrt block output, writes grad wrt the
-  // block input (residual) to r_out.  X = block input, H = hidden activations.
   // lb = the block's LayerNorm backward (dy = grad wrt block output, d_res -> r_out, d_a -> gA);
   // X = block input, H = hidden activations.
   void ffn_bwd(int M, int d, int f, const LnBwd& lb, const void* X, const void* H, int64_t W1, int64_t b1, int64_t W2,
@@ -760,9 +782,9 @@ struct capgen_engine {
     // classifier: dlogits are unscaled (softmax - onehot); grad_scale folds 1/count (+focal)
     fork(s);
     column_sum(a.dlogits, Md, L.V, L.V, 1.f, a.grad_scale, GS(L.bc), act, es2, NSTRIPE, n_small);
-    linear_dw(a.dlogits, L.V, a.D[L.Ld], dd, L.Wc, dd, Md, L.V, dd, a.grad_scale, es2);
+    dw_side(a.dlogits, L.V, a.D[L.Ld], dd, L.Wc, dd, Md, L.V, dd, a.grad_scale, s);
     linear_dx(a.dlogits, L.V, L.Wc, dd, a.gOut, dd, Md, L.V, dd, 0, nullptr, a.grad_scale, s);
-    bucket(L.Wc, L.n_dense - L.Wc, s);  // after the dX GEMM above: it reads Wc
+    bucket(L.Wc, L.n_dense - L.Wc, s);  // flushed after the dX GEMM above: it reads Wc
 
     const int64_t kvld = (int64_t)L.Ld * 2 * dd;
     void* gO = a.gOut;
@@ -803,16 +825,17 @@ struct capgen_engine {
       bucket(w.Wqkv, dec_end(l) - w.Wqkv, s);
       std::swap(gO, gR);  // gO = grad wrt D_l
     }
-    // cross K/V of all decoder blocks -> encoder output (the encoder chain starts here)
-    dw_side(a.gKV, kvld, a.X[L.Le], d, L.Wkv_all, d, Me, L.Ld * 2 * dd, d, nullptr, s);
+    // cross K/V of all decoder blocks -> encoder output (the encoder chain starts here; the
+    // Wkv_all weight gradient is queued after the dX GEMM below, which reads Wkv_all)
     void* eO = gO == a.gOut ? a.gRes : a.gOut;  // the buffer gO is not using
     // decoder embedding: LN(E.Wel^T + PE) (model.py:432-436) -- off the critical path
     {
       const LnBwd lb = dec_emb_lb(gO);
-      flush(s);  // issues the queued cross-K/V weight gradient first
+      flush(s);
       layernorm_bwd(lb, act, es2);
-      linear_dw(a.gAd, dd, a.E, L.dwe, L.Wel, L.dwe, Md, dd, L.dwe, nullptr, es2);
       linear_dx(a.gAd, dd, L.Wel, L.dwe, a.gE, L.dwe, Md, dd, L.dwe, 0, nullptr, nullptr, es2);
+      const DwJob wel{a.gAd, a.E, dd, L.dwe, L.Wel, L.dwe, Md, dd, L.dwe, nullptr};
+      dw_launch(&wel, 1, es2);
       embedding_scatter_add(a.gE, a.ids, Md, L.dwe, cfg.pad_idx, G(L.emb), act, es2);
       // every decoder-side gradient is final here (in es2 order, after the fork above)
       stripe_reduce(GS(L.dec_lng), NSTRIPE, n_small, L.total - L.dec_lng, G(L.dec_lng), 0, es2);
@@ -822,6 +845,7 @@ struct capgen_engine {
     gO = eO;
     gR = a.tmp;
     linear_dx(a.gKV, kvld, L.Wkv_all, d, gO, d, Me, L.Ld * 2 * dd, d, 0, nullptr, nullptr, s);
+    dw_side(a.gKV, kvld, a.X[L.Le], d, L.Wkv_all, d, Me, L.Ld * 2 * dd, d, nullptr, s);
     // the decoder-embedding branch (es2) has been issued: every decoder-side gradient is final
     // the flush of the first bucket follows the dX GEMM above (it reads Wkv_all); es2 then holds
     // every producer of the other three buckets

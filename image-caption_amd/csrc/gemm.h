@@ -28,6 +28,15 @@ struct GemmArgs {
   int64_t colsum_stride = 0;
 };
 
+// Independent GEMMs of one layout launched as ONE grid (tiles problem after problem).
+constexpr int kMaxGroup = 8;
+struct GemmGroup {
+  int n = 0;
+  int start[kMaxGroup + 1] = {};  // first tile of problem i
+  int tiles_n[kMaxGroup] = {};    // column tiles of problem i
+  GemmArgs p[kMaxGroup];
+};
+
 // ta: A stored [K][M] (else [M][K]); tb: B stored [K][N] (else [N][K]).
 void gemm(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t s);
 // allocate the per-device zero page used for out-of-range tiles (call before any bf16 gemm,
@@ -35,6 +44,9 @@ void gemm(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t 
 void gemm_init();
 // experiment hook: force a bf16 GEMM tile/wave/stage variant (0 = heuristic)
 void gemm_set_variant(int v);
+// n <= kMaxGroup independent bf16-operand GEMMs of one layout / output type in one launch
+// (tile variant autotuned per group signature); no beta/colsum/alpha_ptr-free restrictions
+void gemm_grouped(const GemmArgs* probs, int n, DType out, bool ta, bool tb, hipStream_t s);
 // bf16-operand path (gemm_bf16.hip); called by gemm() after argument checks
 void gemm_bf16(const GemmArgs& g, DType out, bool ta, bool tb, hipStream_t s);
 

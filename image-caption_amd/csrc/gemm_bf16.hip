@@ -34,6 +34,7 @@
 #include <map>
 #include <mutex>
 #include <tuple>
+#include <vector>
 
 #include "gemm.h"
 
@@ -154,33 +155,30 @@ __device__ __forceinline__ void store4(TO* p, const float (&v)[4]) {
 
 }  // namespace
 
-template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int STAGES>
-__global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmArgs g, int tiles_n, int nblk,
-                                                                const void* zero, int splitk, float* ws,
-                                                                int* tile_cnt, int group_m) {
-  constexpr int NW = WM * WN;
+// Tile geometry of one variant (shared by the plain and the grouped launch).
+template <bool TA, bool TB, int BM, int BN, int WM, int WN, int STAGES>
+struct TileCfg {
+  static constexpr int NW = WM * WN;
   typedef Op<TA, BM, NW> OA;
   typedef Op<TB, BN, NW> OB;
-  constexpr int SB = OA::BYTES + OB::BYTES;         // bytes per stage
+  static constexpr int SB = OA::BYTES + OB::BYTES;  // LDS bytes per stage
+  static constexpr int SMEM = STAGES * SB;
+};
+
+// One BMxBN output tile (split-K slice `split` of `splitk`) of C = op(A).op(B): the LDS-DMA
+// ring, the MFMA main loop and the epilogue (in-launch split-K combine included).
+template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int STAGES>
+__device__ __forceinline__ void gemm_tile(const GemmArgs& g, int mt, int nt, int tile, int split, int splitk,
+                                          const void* zero, float* ws, int* tile_cnt, char* smem) {
+  typedef TileCfg<TA, TB, BM, BN, WM, WN, STAGES> Cfg;
+  constexpr int NW = Cfg::NW;
+  typedef typename Cfg::OA OA;
+  typedef typename Cfg::OB OB;
+  constexpr int SB = Cfg::SB;                       // bytes per stage
   constexpr int LPT = OA::PER_WAVE + OB::PER_WAVE;  // DMA instructions per wave per K tile
   constexpr int TM = BM / WM, TN = BN / WN;         // per-wave tile
   constexpr int FM = TM / 16, FN = TN / 16;
   static_assert(STAGES >= 2, "need >= 2 stages");
-  __shared__ __attribute__((aligned(1024))) char smem[STAGES * SB];
-
-  // XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> give them adjacent tiles
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nblk >> 3, r8 = nblk & 7;
-  const int slot = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tile = slot / splitk, split = slot % splitk;  // split-K slices of a tile are adjacent
-  // tiles in column-major groups of group_m tile rows: an XCD's contiguous slot range covers a
-  // compact 2D block of the output (fewer distinct A row panels + B column panels per L2)
-  int mt = tile / tiles_n, nt = tile % tiles_n;
-  if (group_m > 1) {
-    const int tiles_m = (g.M + BM - 1) / BM, per = group_m * tiles_n, first = (tile / per) * group_m;
-    const int gsz = min(tiles_m - first, group_m), r = tile % per;
-    mt = first + r % gsz, nt = r / gsz;
-  }
   const int m0 = mt * BM, n0 = nt * BN;
 
   const bf16* __restrict__ A = reinterpret_cast<const bf16*>(g.A);
@@ -337,6 +335,44 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmArgs g, int
       }
     }
   }
+}
+
+// XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> give them adjacent slots
+__device__ __forceinline__ int xcd_slot(int bid, int nblk) {
+  const int xcd = bid & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+}
+
+template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int STAGES>
+__global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmArgs g, int tiles_n, int nblk,
+                                                                const void* zero, int splitk, float* ws,
+                                                                int* tile_cnt, int group_m) {
+  __shared__ __attribute__((aligned(1024))) char smem[TileCfg<TA, TB, BM, BN, WM, WN, STAGES>::SMEM];
+  const int slot = xcd_slot(blockIdx.x, nblk);
+  const int tile = slot / splitk, split = slot % splitk;  // split-K slices of a tile are adjacent
+  // tiles in column-major groups of group_m tile rows: an XCD's contiguous slot range covers a
+  // compact 2D block of the output (fewer distinct A row panels + B column panels per L2)
+  int mt = tile / tiles_n, nt = tile % tiles_n;
+  if (group_m > 1) {
+    const int tiles_m = (g.M + BM - 1) / BM, per = group_m * tiles_n, first = (tile / per) * group_m;
+    const int gsz = min(tiles_m - first, group_m), r = tile % per;
+    mt = first + r % gsz, nt = r / gsz;
+  }
+  gemm_tile<TO, TA, TB, BM, BN, WM, WN, STAGES>(g, mt, nt, tile, split, splitk, zero, ws, tile_cnt, smem);
+}
+
+// Grouped launch: up to kMaxGroup independent GEMMs of one layout (e.g. every weight gradient
+// of a transformer block), each with its own M/N/pointers, tiles laid out problem after
+// problem; one launch instead of one per weight, and a grid that fills the chip.
+template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int STAGES>
+__global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_grouped_kernel(GemmGroup gg, int nblk, const void* zero) {
+  __shared__ __attribute__((aligned(1024))) char smem[TileCfg<TA, TB, BM, BN, WM, WN, STAGES>::SMEM];
+  const int slot = xcd_slot(blockIdx.x, nblk);
+  int q = 0;
+  while (q + 1 < gg.n && slot >= gg.start[q + 1]) ++q;
+  const int tile = slot - gg.start[q];
+  const int mt = tile / gg.tiles_n[q], nt = tile % gg.tiles_n[q];
+  gemm_tile<TO, TA, TB, BM, BN, WM, WN, STAGES>(gg.p[q], mt, nt, tile, 0, 1, zero, nullptr, nullptr, smem);
 }
 
 // split-K f32 workspaces, one per stream (GEMMs on different streams may run concurrently)
@@ -517,6 +553,13 @@ static Choice tune(const GemmArgs& g, hipStream_t s) {
 template <typename TO, bool TA, bool TB>
 static void launch_bf16_tiles(const GemmArgs& g, hipStream_t s) {
   Choice c{g_variant % 100, std::max(1, g_variant / 100)};  // forced: variant + 100 * splitk
+  if (TA && c.variant == 0) {  // experiment knob: weight-gradient (TN) GEMMs on a fixed variant
+    static const int dwv = [] {
+      const char* e = std::getenv("CAPGEN_DW_VARIANT");
+      return e ? std::atoi(e) : 0;
+    }();
+    if (dwv) c = Choice{dwv % 100, std::max(1, dwv / 100)};
+  }
   if (c.splitk > 1) ensure_ws(s, splitk_bytes(g, c.splitk));
   if (c.variant == 0) {
     c.variant = heuristic_variant(g);
@@ -549,6 +592,117 @@ static void launch_bf16_layout(const GemmArgs& g, bool ta, bool tb, hipStream_t 
   else if (!ta && tb) launch_bf16_tiles<TO, false, true>(g, s);
   else if (ta && !tb) launch_bf16_tiles<TO, true, false>(g, s);
   else launch_bf16_tiles<TO, true, true>(g, s);
+}
+
+// ---- grouped launch ---------------------------------------------------------------------
+template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int ST>
+static void launch_group_cfg(const GemmArgs* ps, int n, hipStream_t s) {
+  int dev = 0;
+  CAPGEN_HIP(hipGetDevice(&dev));
+  GemmGroup gg;
+  gg.n = n;
+  int tot = 0;
+  for (int i = 0; i < n; ++i) {
+    const int tn = (ps[i].N + BN - 1) / BN, tm = (ps[i].M + BM - 1) / BM;
+    gg.start[i] = tot, gg.tiles_n[i] = tn, gg.p[i] = ps[i];
+    tot += tn * tm;
+  }
+  gg.start[n] = tot;
+  gemm_bf16_grouped_kernel<TO, TA, TB, BM, BN, WM, WN, ST><<<tot, 64 * WM * WN, 0, s>>>(gg, tot, g_zero_page[dev]);
+}
+
+// the variants worth a grouped launch (many tiles already: no split-K)
+constexpr int kGroupVariants[] = {6, 20, 17, 18, 19, 4, 8, 1, 3, 10};
+
+template <typename TO, bool TA, bool TB>
+static void launch_group_variant(int v, const GemmArgs* ps, int n, hipStream_t s) {
+  switch (v) {
+    case 1: return launch_group_cfg<TO, TA, TB, 128, 128, 2, 2, 3>(ps, n, s);
+    case 3: return launch_group_cfg<TO, TA, TB, 128, 128, 2, 2, 2>(ps, n, s);
+    case 4: return launch_group_cfg<TO, TA, TB, 128, 64, 2, 2, 2>(ps, n, s);
+    case 6: return launch_group_cfg<TO, TA, TB, 64, 64, 2, 2, 2>(ps, n, s);
+    case 8: return launch_group_cfg<TO, TA, TB, 128, 64, 4, 2, 2>(ps, n, s);
+    case 10: return launch_group_cfg<TO, TA, TB, 128, 128, 4, 4, 2>(ps, n, s);
+    case 17: return launch_group_cfg<TO, TA, TB, 32, 64, 2, 2, 2>(ps, n, s);
+    case 18: return launch_group_cfg<TO, TA, TB, 64, 32, 2, 2, 2>(ps, n, s);
+    case 19: return launch_group_cfg<TO, TA, TB, 32, 32, 2, 2, 2>(ps, n, s);
+    case 20: return launch_group_cfg<TO, TA, TB, 64, 64, 4, 2, 2>(ps, n, s);
+    default: throw Error("gemm_grouped: unknown variant");
+  }
+}
+
+std::map<std::vector<int>, int> g_group_tuned;
+
+template <typename TO, bool TA, bool TB>
+static void launch_group(const GemmArgs* ps, int n, hipStream_t s) {
+  std::vector<int> key{TA, TB, (int)sizeof(TO)};
+  for (int i = 0; i < n; ++i) key.insert(key.end(), {ps[i].M, ps[i].N, ps[i].K});
+  int v = g_variant % 100;
+  if (v == 0) {
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    auto it = g_group_tuned.find(key);
+    if (it != g_group_tuned.end()) {
+      v = it->second;
+    } else {
+      v = kGroupVariants[0];
+      hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+      CAPGEN_HIP(hipStreamIsCapturing(s, &st));
+      if (st == hipStreamCaptureStatusNone && autotune_enabled()) {
+        // time each variant on scratch outputs (inputs untouched, beta forced to 0)
+        std::vector<GemmArgs> t(ps, ps + n);
+        std::vector<void*> scratch(n);
+        for (int i = 0; i < n; ++i) {
+          CAPGEN_HIP(hipMalloc(&scratch[i], (size_t)t[i].M * t[i].ldc * sizeof(TO)));
+          t[i].C = scratch[i], t[i].beta = 0, t[i].colsum = nullptr;
+        }
+        hipEvent_t e0, e1;
+        CAPGEN_HIP(hipEventCreate(&e0));
+        CAPGEN_HIP(hipEventCreate(&e1));
+        float best = 1e30f;
+        for (int cand : kGroupVariants) {
+          launch_group_variant<TO, TA, TB>(cand, t.data(), n, s);
+          CAPGEN_HIP(hipEventRecord(e0, s));
+          for (int r = 0; r < 3; ++r) launch_group_variant<TO, TA, TB>(cand, t.data(), n, s);
+          CAPGEN_HIP(hipEventRecord(e1, s));
+          CAPGEN_HIP(hipEventSynchronize(e1));
+          float ms = 0.f;
+          CAPGEN_HIP(hipEventElapsedTime(&ms, e0, e1));
+          if (ms < best) best = ms, v = cand;
+        }
+        CAPGEN_HIP(hipEventDestroy(e0));
+        CAPGEN_HIP(hipEventDestroy(e1));
+        for (void* p : scratch) CAPGEN_HIP(hipFree(p));
+        g_group_tuned[key] = v;
+        if (std::getenv("CAPGEN_AUTOTUNE_LOG"))
+          std::fprintf(stderr, "[capgen gemm] group of %d (M=%d N=%d K=%d first) -> %s (%.2f us)\n", n, ps[0].M,
+                       ps[0].N, ps[0].K, kVariantName[v], best * 1e3f / 3);
+      }
+    }
+  }
+  launch_group_variant<TO, TA, TB>(v, ps, n, s);
+}
+
+void gemm_grouped(const GemmArgs* ps, int n, DType out, bool ta, bool tb, hipStream_t s) {
+  require(n >= 1 && n <= kMaxGroup, "gemm_grouped: 1..kMaxGroup problems");
+  int dev = 0;
+  CAPGEN_HIP(hipGetDevice(&dev));
+  require(g_zero_page[dev] != nullptr, "gemm: gemm_init() not called on this device");
+  for (int i = 0; i < n; ++i) {
+    const GemmArgs& g = ps[i];
+    require(g.M > 0 && g.N > 0 && g.K > 0 && g.N % 4 == 0 && g.ldc % 4 == 0 && (g.aux == nullptr || g.ldaux % 4 == 0),
+            "gemm_grouped: bad problem shape");
+    require(((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0, "gemm_grouped: operands must be 16-B aligned");
+  }
+  if (out == DType::F32) {
+    if (ta && tb) launch_group<float, true, true>(ps, n, s);
+    else if (!ta && tb) launch_group<float, false, true>(ps, n, s);
+    else throw Error("gemm_grouped: layout not instantiated");
+  } else {
+    if (!ta && tb) launch_group<bf16, false, true>(ps, n, s);
+    else if (!ta && !tb) launch_group<bf16, false, false>(ps, n, s);
+    else throw Error("gemm_grouped: layout not instantiated");
+  }
+  CAPGEN_HIP(hipGetLastError());
 }
 
 void gemm_set_variant(int v) { g_variant = v; }

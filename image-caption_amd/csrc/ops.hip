@@ -502,13 +502,6 @@ void adam_prepare(int64_t* step, float lr, float b1, float b2, float* scal, hipS
   CAPGEN_HIP(hipGetLastError());
 }
 
-__device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, float b1c, float b2, float b2c,
-                                         float eps, float neg_step, float bc2s) {
-  m = m + b1c * (g - m);                      // exp_avg.lerp_(grad, 1 - beta1)
-  v = v * b2 + b2c * (g * g);                 // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
-  const float denom = sqrtf(v) / bc2s + eps;  // (exp_avg_sq.sqrt() / bc2_sqrt).add_(eps)
-  p = p + (neg_step * m) / denom;             // param.addcdiv_(exp_avg, denom, value=-step_size)
-}
 
 __global__ void __launch_bounds__(256) adam_kernel(float4* __restrict__ p, const float4* __restrict__ g,
                                                    float4* __restrict__ m, float4* __restrict__ v, size_t n4,

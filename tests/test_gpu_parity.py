@@ -221,6 +221,79 @@ def test_bf16_train_mode_matches_fp32_with_dropout():
         assert rel < 0.2, (n, rel)
 
 
+def test_grouped_weight_gradients_match_single_launches_bf16(monkeypatch):
+    """bf16 weight gradients of one block computed by ONE grouped launch (default) equal the
+    per-weight launches (CAPGEN_GROUP_DW=0) up to f32 summation order (split-K choices)."""
+    cfg, seed, z = load_fixture("c2s")
+    f, p, c = _inputs(z)
+    monkeypatch.setenv("CAPGEN_GROUP_DW", "0")
+    a = _engine(cfg, seed, dtype="bf16", dropout=0.3)
+    monkeypatch.delenv("CAPGEN_GROUP_DW")
+    b = _engine(cfg, seed, dtype="bf16", dropout=0.3)
+    for e in (a, b):
+        e.set_training(True)
+        e.set_rng_seed(5)
+        e.forward(f, p, c)
+        e.backward()
+    ga, gb = a.grads_state_dict(), b.grads_state_dict()
+    for n in ga:
+        x, y = ga[n].double(), gb[n].double()
+        assert ((x - y).norm() / (x.norm() + 1e-12)).item() < 1e-4, n
+
+
+def test_grouped_weight_gradients_match_single_launches_bf16(monkeypatch):
+    """bf16 weight gradients of one block computed by ONE grouped launch (default) equal the
+    per-weight launches (CAPGEN_GROUP_DW=0) up to f32 summation order (split-K choices)."""
+    cfg, seed, z = load_fixture("c2s")
+    f, p, c = _inputs(z)
+    monkeypatch.setenv("CAPGEN_GROUP_DW", "0")
+    a = _engine(cfg, seed, dtype="bf16", dropout=0.3)
+    monkeypatch.delenv("CAPGEN_GROUP_DW")
+    b = _engine(cfg, seed, dtype="bf16", dropout=0.3)
+    for e in (a, b):
+        e.set_training(True)
+        e.set_rng_seed(5)
+        e.forward(f, p, c)
+        e.backward()
+    ga, gb = a.grads_state_dict(), b.grads_state_dict()
+    for n in ga:
+        x, y = ga[n].double(), gb[n].double()
+        assert ((x - y).norm() / (x.norm() + 1e-12)).item() < 1e-4, n
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_fused_adam_train_step_equals_unfused_bf16(graph):
+    """bf16 train_step applies Adam inside the grouped weight-gradient launches (single process);
+    it must equal forward -> backward -> adam_step (separate Adam pass over the whole arena):
+    after one step every Linear weight bit-identical (same gradients, same Adam arithmetic);
+    LayerNorm/bias/embedding parameters up to f32-atomic summation order."""
+    cfg, seed, z = load_fixture("c2s")
+    f, p, c = _inputs(z)
+    a = _engine(cfg, seed, dtype="bf16")
+    b = _engine(cfg, seed, dtype="bf16")
+    for e in (a, b):
+        e.set_training(False)
+    a.set_graph(graph)
+    la = a.train_step(f, p, c).clone()
+    lb = b.forward(f, p, c).clone()
+    b.backward()
+    b.adam_step()
+    torch.cuda.synchronize()
+    assert la.item() == lb.item()
+    sa, sb = a.state_dict(False), b.state_dict(False)
+    for k in sa:
+        if sa[k].dim() == 2 and k != "decoder.word_embedding.weight":  # every Linear weight
+            assert torch.equal(sa[k], sb[k]), k
+        torch.testing.assert_close(sa[k], sb[k], atol=1e-5, rtol=0, msg=k)
+    for _ in range(2):  # later steps: losses agree (params drift in the last bits, see above)
+        la = a.train_step(f, p, c).clone()
+        lb = b.forward(f, p, c).clone()
+        b.backward()
+        b.adam_step()
+        torch.cuda.synchronize()
+        assert abs(la.item() - lb.item()) < 1e-4 * abs(lb.item())
+
+
 def test_dropout_backward_directional_derivative_fp32():
     """Train-mode (dropout on) gradient vs a central finite difference of the same
     dropout mask (RNG reset before each forward)."""
