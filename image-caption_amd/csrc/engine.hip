@@ -713,11 +713,13 @@ struct capgen_engine {
   // Buckets are issued in reverse layer order: 12-20 MB each at C2, one per block.
   // sync: first flush (es2 waits for s, queued dW issued); sync=false when es2 already holds
   // every producer of the bucket's gradients (consecutive buckets after one flush)
+  // from_s: every producer of the bucket's gradients ran on s (no flush, ec waits for s)
   bool bstep = false;
-  void bucket(int64_t off, int64_t n, hipStream_t s, bool sync = true) {
-    if (sync) flush(s);
+  void bucket(int64_t off, int64_t n, hipStream_t s, bool sync = true, bool from_s = false) {
+    if (sync && !from_s) flush(s);
     if (!bstep) return;
-    dep(es2, ec, ev_b2);
+    if (from_s) dep(s, ec, ev_b1);
+    else dep(es2, ec, ev_b2);
     if (comm) NCCL_CHECK(ncclAllReduce(grads + off, grads + off, (size_t)n, ncclFloat, ncclSum, comm, ec));
     adam_range(off, n, ec);
   }
@@ -874,15 +876,18 @@ struct capgen_engine {
       linear_dx(gb.gQKV, 3 * d, w.Wqkv, d, gO, d, Me, 3 * d, d, 1, nullptr, nullptr, s);  // gO = grad wrt X_l
       bucket(w.Wqkv, enc_end(l) - w.Wqkv, s);
     }
-    {
-      layernorm_bwd(enc_emb_lb(gO), act, s);
-      dw_side(a.gAe, d, a.Aenc, L.Kp, L.enc_emb_W, L.Kp, Me, d, L.Kp, nullptr, s);
-    }
-    join(s);
+    // the tail of the step's dependency chain: the encoder-embedding LayerNorm backward and
+    // weight gradient, then its Adam, which the next forward's first GEMM needs -- on the
+    // critical stream, so it does not queue behind the weight-gradient groups still on es2
+    layernorm_bwd(enc_emb_lb(gO), act, s);
+    const DwJob emb{a.gAe, a.Aenc, d, L.Kp, L.enc_emb_W, L.Kp, Me, d, L.Kp, nullptr};
+    dw_launch(&emb, 1, s);
+    // every encoder LayerNorm/bias partial was accumulated on s
     stripe_reduce(GS(L.enc_lng), NSTRIPE, n_small, L.dec_lng - L.enc_lng, G(L.enc_lng), 0, s);
+    bucket(0, L.enc[0].Wqkv, s, false, true);                     // feature/position embedding
+    bucket(L.enc_lng, L.dec_lng - L.enc_lng, s, false, true);      // encoder LN / biases
+    join(s);
     if (bstep) {
-      bucket(0, L.enc[0].Wqkv, s);                        // feature/position embedding
-      bucket(L.enc_lng, L.dec_lng - L.enc_lng, s, false);  // encoder LN / biases
       dep(ec, s, ev_cj);
       bstep = false;
     }
