@@ -67,7 +67,7 @@ def dominant_gemm(eng, steps=50):
     e1.synchronize()
     ms = e0.elapsed_time(e1) / steps
     flops = 2.0 * M * Nn * K
-    return {"kernel": "gemm_kernel<bf16,bf16,NT> enc FFN-up 2304x2048x512 (+bias,relu)",
+    return {"kernel": "gemm_bf16_kernel (NT) enc FFN-up 2304x2048x512 (+bias,relu), autotuned variant",
             "avg_us": round(ms * 1e3, 2), "achieved": round(flops / (ms * 1e-3) / 1e12, 1), "unit": "TFLOP/s",
             "frac": round(flops / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4)}
 

@@ -53,6 +53,13 @@ def main():
     if "--steps" in sys.argv:
         K = int(sys.argv[sys.argv.index("--steps") + 1])
     rows = sorted(load(path), key=lambda r: r["s"])
+    if "--dominant" in sys.argv:
+        # bench.py's dominant_gemm(): the last 50 GEMM launches of the run (after 10 warm-ups)
+        dom = [r for r in rows if "gemm_bf16_kernel" in r["name"]][-50:]
+        avg = sum(r["e"] - r["s"] for r in dom) / len(dom) / 1e3
+        print(f"dominant GEMM (bench.py dominant_gemm, last {len(dom)} launches): trace average {avg:.2f} us, "
+              f"grid {dom[-1]['grid']}/{dom[-1]['wg']}, {short(dom[-1]['name'])}")
+        return
     marks = [i for i, r in enumerate(rows) if "adam_prep_kernel" in r["name"]]
     K = min(K, len(marks) - 1)
     sel = rows[marks[-K - 1]:marks[-1]]
