@@ -455,11 +455,70 @@ __global__ void __launch_bounds__(256) ce_kernel(const float* __restrict__ logit
   }
   if (threadIdx.x == 0) loss_row[m] = (logf(se) + mx) - x[y];
 }
+// Register-resident variant (V % 4 == 0, V <= 1024 * NV4): the row is loaded ONCE as float4s
+// (every load in flight together: one memory round trip instead of three dependent passes),
+// max / sum-exp / gradient are computed from registers.
+template <typename T, int NV4>
+__global__ void __launch_bounds__(256) ce_reg_kernel(const float* __restrict__ logits, const int32_t* __restrict__ tgt,
+                                                     int V, int pad, float* __restrict__ loss_row, T* __restrict__ dl) {
+  __shared__ float sh[4];
+  const int m = blockIdx.x, V4 = V >> 2;
+  const float4* x = reinterpret_cast<const float4*>(logits + (int64_t)m * V);
+  T* g = dl + (int64_t)m * V;
+  const int y = tgt[m];
+  if (y == pad) {
+    for (int c = threadIdx.x; c < V; c += 256) g[c] = from_f<T>(0.f);
+    if (threadIdx.x == 0) loss_row[m] = 0.f;
+    return;
+  }
+  float4 v[NV4];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < NV4; ++u) {
+    const int c4 = threadIdx.x + 256 * u;
+    v[u] = c4 < V4 ? x[c4] : float4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  }
+#pragma unroll
+  for (int u = 0; u < NV4; ++u) mx = fmaxf(mx, fmaxf(fmaxf(v[u].x, v[u].y), fmaxf(v[u].z, v[u].w)));
+  mx = block_max(mx, sh);
+  float se = 0.f;
+#pragma unroll
+  for (int u = 0; u < NV4; ++u) {
+    v[u].x = expf(v[u].x - mx), v[u].y = expf(v[u].y - mx), v[u].z = expf(v[u].z - mx), v[u].w = expf(v[u].w - mx);
+    se += (v[u].x + v[u].y) + (v[u].z + v[u].w);
+  }
+  se = block_sum(se, sh);
+  const float inv = 1.f / se;
+#pragma unroll
+  for (int u = 0; u < NV4; ++u) {
+    const int c4 = threadIdx.x + 256 * u;
+    if (c4 >= V4) continue;
+    const int c = 4 * c4;
+    float o[4] = {v[u].x * inv, v[u].y * inv, v[u].z * inv, v[u].w * inv};
+    if (y >= c && y < c + 4) o[y - c] -= 1.f;
+    store_f<T, 4>(g + c, o);
+  }
+  if (threadIdx.x == 0) loss_row[m] = (logf(se) + mx) - logits[(int64_t)m * V + y];
+}
+
+template <typename T>
+static void ce_launch(const float* logits, const int32_t* tgt, int M, int V, int pad, float* loss_row, T* dl,
+                      hipStream_t s) {
+  if (V % 4 == 0 && V <= 1024 * 16) {
+    const int nv4 = (V / 4 + 255) / 256;
+    if (nv4 <= 4) ce_reg_kernel<T, 4><<<M, 256, 0, s>>>(logits, tgt, V, pad, loss_row, dl);
+    else if (nv4 <= 8) ce_reg_kernel<T, 8><<<M, 256, 0, s>>>(logits, tgt, V, pad, loss_row, dl);
+    else if (nv4 <= 10) ce_reg_kernel<T, 10><<<M, 256, 0, s>>>(logits, tgt, V, pad, loss_row, dl);
+    else ce_reg_kernel<T, 16><<<M, 256, 0, s>>>(logits, tgt, V, pad, loss_row, dl);
+  } else {
+    ce_kernel<T><<<M, 256, 0, s>>>(logits, tgt, V, pad, loss_row, dl);
+  }
+}
 void cross_entropy_rows(const float* logits, const int32_t* tgt, int M, int V, int pad, float* loss_row, void* dl,
                         DType t, hipStream_t s) {
   if (M <= 0) return;
-  if (t == DType::F32) ce_kernel<float><<<M, 256, 0, s>>>(logits, tgt, V, pad, loss_row, (float*)dl);
-  else ce_kernel<bf16><<<M, 256, 0, s>>>(logits, tgt, V, pad, loss_row, (bf16*)dl);
+  if (t == DType::F32) ce_launch<float>(logits, tgt, M, V, pad, loss_row, (float*)dl, s);
+  else ce_launch<bf16>(logits, tgt, M, V, pad, loss_row, (bf16*)dl, s);
   CAPGEN_HIP(hipGetLastError());
 }
 

@@ -10,6 +10,7 @@ step in start order with their queue, duration and the gap before them on that q
 import collections
 import csv
 import os
+import re
 import sqlite3
 import sys
 
@@ -26,6 +27,12 @@ def load(path):
 
 
 def short(n):
+    if "gemm_bf16_kernel" in n and "<" not in n:  # mangled: ...kernelI<TO>Lb<TA>ELb<TB>ELi<BM>E...
+        m = re.search(r"gemm_bf16_kernelI(DF16b|f)Lb(\d)ELb(\d)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", n)
+        if m:
+            to, ta, tb, bm, bn, wm, wn, st = m.groups()
+            lay = {("0", "0"): "NT", ("0", "1"): "NN", ("1", "1"): "TN"}.get((ta, tb), ta + tb)
+            return f"gemm {lay} {'bf16' if to == 'DF16b' else 'f32'} {bm}x{bn} w{int(wm) * int(wn)} s{st}"
     if "gemm_bf16_kernel" in n:
         return "gemm " + n[n.find("<"):n.find(">") + 1][:60]
     n = n.split("(")[0]
