@@ -109,6 +109,13 @@ elif __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "sk":
                 print(f"M={M} N={N} K={K} ta={ta} tb={tb} v={v} sk={sk}: {us:7.2f} us "
                       f"{2 * M * N * K / us / 1e6:6.1f} TF/s  rel.diff {err:.1e}", flush=True)
     _lib.check(lib.capgen_debug_gemm_variant(0))
+elif __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "nnnt":
+    # forward (NT) vs input-gradient (NN) layout on the step's shapes, autotuned variant, alone
+    for (M, N, K) in [(2304, 2048, 512), (2304, 512, 2048), (2304, 1536, 512), (2304, 512, 1536), (2304, 512, 512),
+                      (1216, 2048, 512), (1216, 512, 2048), (1216, 1536, 512), (1216, 512, 1536), (1216, 512, 512),
+                      (1216, 512, 10000)]:
+        for tb in (0, 1):
+            run(M, N, K, 0, tb, 0)
 elif __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "sweep":
     sweep()
 elif __name__ == "__main__":
