@@ -138,6 +138,34 @@ int main() {
     CK(hipStreamSynchronize(s));
     std::printf("host enqueue fork/join: %.2f us/iter\n", std::chrono::duration<double, std::micro>(t1 - t0).count() / K);
   }
+  // what does a cross-stream signal cost the SIGNALLING stream? (no waits: a chain of 1024-WG
+  // kernels on s with a marker after every kernel)
+  {
+    hipEvent_t eflag[3];
+    const unsigned flags[3] = {hipEventDisableTiming, hipEventDisableTiming | hipEventReleaseToDevice,
+                               hipEventDisableTiming | hipEventDisableSystemFence};
+    const char* names[3] = {"default", "release-to-device", "no-system-fence"};
+    for (int f = 0; f < 3; ++f) {
+      CK(hipEventCreateWithFlags(&eflag[f], flags[f]));
+      std::printf("eager kernel+record %-17s: %.2f us/iter\n", names[f], time_it(s, 3, [&] {
+        for (int i = 0; i < K; ++i) {
+          tiny<<<1024, 256, 0, s>>>(p);
+          CK(hipEventRecord(eflag[f], s));
+        }
+      }) / K);
+    }
+    uint32_t* sig = nullptr;
+    if (hipExtMallocWithFlags((void**)&sig, 4096, hipMallocSignalMemory) == hipSuccess) {
+      std::printf("eager kernel+writeValue32        : %.2f us/iter\n", time_it(s, 3, [&] {
+        for (int i = 0; i < K; ++i) {
+          tiny<<<1024, 256, 0, s>>>(p);
+          CK(hipStreamWriteValue32(s, sig, (uint32_t)i, 0));
+        }
+      }) / K);
+    } else {
+      std::printf("signal memory unavailable\n");
+    }
+  }
   // host price of the runtime calls a launch wrapper tends to make
   auto host_us = [&](const char* what, const std::function<void()>& f) {
     const int R = 2000;
