@@ -720,6 +720,10 @@ struct capgen_engine {
     if (!bstep) return;
     if (from_s) dep(s, ec, ev_b1);
     else dep(es2, ec, ev_b2);
+    bucket_update(off, n);
+  }
+  // the bucket's all-reduce (DP) + Adam on the bucket stream (its producers already waited for)
+  void bucket_update(int64_t off, int64_t n) {
     if (comm) NCCL_CHECK(ncclAllReduce(grads + off, grads + off, (size_t)n, ncclFloat, ncclSum, comm, ec));
     adam_range(off, n, ec);
   }
@@ -879,13 +883,19 @@ struct capgen_engine {
     // the tail of the step's dependency chain: the encoder-embedding LayerNorm backward and
     // weight gradient, then its Adam, which the next forward's first GEMM needs -- on the
     // critical stream, so it does not queue behind the weight-gradient groups still on es2
+    // (a single GEMM: the plain launch with its autotuned split-K, K = B*N = 2304 deep)
     layernorm_bwd(enc_emb_lb(gO), act, s);
-    const DwJob emb{a.gAe, a.Aenc, d, L.Kp, L.enc_emb_W, L.Kp, Me, d, L.Kp, nullptr};
-    dw_launch(&emb, 1, s);
-    // every encoder LayerNorm/bias partial was accumulated on s
-    stripe_reduce(GS(L.enc_lng), NSTRIPE, n_small, L.dec_lng - L.enc_lng, G(L.enc_lng), 0, s);
-    bucket(0, L.enc[0].Wqkv, s, false, true);                     // feature/position embedding
-    bucket(L.enc_lng, L.dec_lng - L.enc_lng, s, false, true);      // encoder LN / biases
+    linear_dw(a.gAe, d, a.Aenc, L.Kp, L.enc_emb_W, L.Kp, Me, d, L.Kp, nullptr, s);
+    // every encoder LayerNorm/bias partial was accumulated on s; in step mode the fold and the
+    // last two buckets (feature/position embedding, encoder LN / biases) run on the bucket
+    // stream behind ONE event (each event record costs the critical stream ~5 us)
+    const hipStream_t tail = bstep ? ec : s;
+    if (bstep) dep(s, ec, ev_b1);
+    stripe_reduce(GS(L.enc_lng), NSTRIPE, n_small, L.dec_lng - L.enc_lng, G(L.enc_lng), 0, tail);
+    if (bstep) {
+      bucket_update(0, L.enc[0].Wqkv);                   // feature/position embedding
+      bucket_update(L.enc_lng, L.dec_lng - L.enc_lng);   // encoder LN / biases
+    }
     join(s);
     if (bstep) {
       dep(ec, s, ev_cj);
