@@ -165,6 +165,10 @@ struct TileCfg {
   static constexpr int SMEM = STAGES * SB;
 };
 
+template <typename TO, int FM, int FN, int TM, int TN>
+__device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&acc)[FM][FN], int m0, int n0, int wm,
+                                              int wn, int lane, float alpha);
+
 // One BMxBN output tile (split-K slice `split` of `splitk`) of C = op(A).op(B): the LDS-DMA
 // ring, the MFMA main loop and the epilogue (in-launch split-K combine included).
 template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int STAGES>
@@ -279,6 +283,14 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int mt, int nt, int
         acc[i][j] = sum;
       }
   }
+  tile_epilogue<TO, FM, FN, TM, TN>(g, acc, m0, n0, wm, wn, lane, alpha);
+}
+
+// Store one tile's accumulators: alpha, bias, ReLU' mask (aux), ReLU, accumulate (beta),
+// conversion, column sums.  Lane holds C[m = mb + (lane&15)][n = nb + 4*(lane>>4) + 0..3].
+template <typename TO, int FM, int FN, int TM, int TN>
+__device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&acc)[FM][FN], int m0, int n0, int wm,
+                                              int wn, int lane, float alpha) {
   TO* __restrict__ C = reinterpret_cast<TO*>(g.C);
   const bf16* __restrict__ aux = reinterpret_cast<const bf16*>(g.aux);
   const int fr = lane & 15, fq = lane >> 4;
