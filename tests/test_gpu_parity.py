@@ -577,3 +577,23 @@ def test_edge_shapes_bf16_close_to_oracle(case):
     torch.cuda.synchronize()
     assert abs(lg.item() - lo.item()) < 1e-2 * abs(lo.item()), (case, lg.item(), lo.item())
     assert all(torch.isfinite(v).all() for v in e.grads_state_dict().values())
+
+
+@pytest.mark.parametrize("case", ["min", "ragged", "maxN", "onevalid"])
+def test_edge_shapes_decode_fp32_match_oracle(case):
+    """Greedy ids bit-exact (and cross-attention maps within 1e-4) and beam-3 ids exact vs the
+    CPU oracle on the edge shapes (one image with one region, 64 regions, ragged regions)."""
+    import sys, os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle import capgen_oracle as O
+    from capgen.config import preset
+    cfg = preset("C1")
+    f, p, _ = _edge_batch(case, cfg.encode_dim_features, cfg.encode_dim_positions, cfg.num_vocab)
+    P = O.make_params(fixture_state_dict(cfg, 0, with_buffer=False), requires_grad=False)
+    ids_ref, attn_ref = O.greedy(P, cfg, f, p)
+    e = _engine(cfg, 0)
+    e.set_training(False)
+    ids, attn = e.greedy(f.to(DEV), p.to(DEV))
+    np.testing.assert_array_equal(ids.cpu().numpy(), ids_ref.numpy())
+    np.testing.assert_allclose(attn.cpu().numpy(), np.stack(attn_ref), atol=1e-4)
+    np.testing.assert_array_equal(e.beam(f.to(DEV), p.to(DEV), 3).cpu().numpy(), O.beam(P, cfg, f, p, 3).numpy())
