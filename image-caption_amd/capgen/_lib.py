@@ -76,6 +76,8 @@ _SIGS = {
     "capgen_dp_unique_id": (C.c_int, [C.c_char_p]),
     "capgen_dp_init": (C.c_int, [_P, C.c_char_p, C.c_int, C.c_int]),
     "capgen_dp_set_global_count": (C.c_int, [_P, C.c_float]),
+    "capgen_scst_rewards": (C.c_int, [_P, C.c_int64, _P, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                      C.c_int64, C.c_double, C.c_double, _P]),
 }
 EXPORTED = tuple(_SIGS)
 

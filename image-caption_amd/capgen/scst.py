@@ -144,20 +144,46 @@ def self_cider_single(res_one: list) -> float:
     return 0.0
 
 
+def native_rewards(target, sample, start_id, end_id, null_id, dot_id, cider_w, bleu_w):
+    """cider_w * CIDEr-D + bleu_w * BLEU-4 per image, computed by libcapgen's host code
+    (csrc/scst_host.cpp: the arithmetic of CiderD(df='corpus') and Bleu(4) above on token ids)."""
+    import ctypes as C
+    from . import _lib
+    lib = _lib.load()
+    t = np.ascontiguousarray(target, dtype=np.int64)
+    s = np.ascontiguousarray(sample, dtype=np.int64)
+    assert t.ndim == 2 and t.shape == s.shape
+    B, L = t.shape
+    out = np.empty(B, dtype=np.float64)
+    _lib.check(lib.capgen_scst_rewards(t.ctypes.data_as(C.c_void_p), L, s.ctypes.data_as(C.c_void_p), L, B, L,
+                                       int(start_id), int(end_id), int(null_id), int(dot_id), float(cider_w),
+                                       float(bleu_w), out.ctypes.data_as(C.c_void_p)))
+    return out
+
+
 class RewardScorer:
-    """StructureCriterion.get_scores + the entropy / self-CIDEr terms (loss.py:115-181)."""
+    """StructureCriterion.get_scores + the entropy / self-CIDEr terms (loss.py:115-181).
+
+    native=True (default with corpus document frequencies): the rewards come from libcapgen's
+    host code on token ids (`native_rewards`), the Python CiderD/Bleu above being the
+    restatement it is tested against (tests/test_scst.py)."""
 
     def __init__(self, idx_to_word, cider_reward_weight=1.0, bleu_reward_weight=1.0, entropy_reward_weight=1.0,
-                 self_cider_reward_weight=1.0, df="corpus"):
+                 self_cider_reward_weight=1.0, df="corpus", native=True):
         from .utils import decode_captions
         self._decode = lambda ids: decode_captions(ids, idx_to_word)
         self.cider_w, self.bleu_w = cider_reward_weight, bleu_reward_weight
         self.entropy_w, self.self_cider_w = entropy_reward_weight, self_cider_reward_weight
         self.ciderD = CiderD(df=df)
         self.bleu = Bleu(4)
+        w2i = {w: i for i, w in (idx_to_word.items() if isinstance(idx_to_word, dict) else enumerate(idx_to_word))}
+        self._ids = (w2i.get("<START>", 1), w2i.get("<END>", 2), w2i.get("<NULL>", 0), w2i.get(".", -1))
+        self.native = native and isinstance(df, str) and df == "corpus"
 
     def scores(self, target, sample):
         """target = caption[:, 1:] [B, L], sample [B, L] (host int arrays) -> reward [B]."""
+        if self.native:
+            return native_rewards(target, sample, *self._ids, self.cider_w, self.bleu_w)
         res = self._decode(np.asarray(sample))
         gts = self._decode(np.asarray(target))
         res_d = {i: [res[i]] for i in range(len(res))}

@@ -1273,6 +1273,11 @@ struct capgen_engine {
 // =========================================================================================
 // C ABI
 // =========================================================================================
+namespace capgen {
+void scst_rewards(const int64_t* target, int64_t target_ld, const int64_t* sample, int64_t sample_ld, int B, int L,
+                  int start_id, int end_id, int null_id, int64_t dot_id, double cider_w, double bleu_w, double* out);
+}
+
 namespace {
 
 template <class F>
@@ -1608,6 +1613,14 @@ int capgen_rl_finish(capgen_t* h, const float* scores, float structure_loss_weig
   return guarded([&] {
     set_device(h);
     h->rl_finish(scores, structure_loss_weight, loss_out, train != 0, (hipStream_t)stream);
+  });
+}
+
+int capgen_scst_rewards(const int64_t* target, int64_t target_ld, const int64_t* sample, int64_t sample_ld, int B,
+                        int L, int start_id, int end_id, int null_id, int64_t dot_id, double cider_w, double bleu_w,
+                        double* out) {
+  return guarded([&] {
+    scst_rewards(target, target_ld, sample, sample_ld, B, L, start_id, end_id, null_id, dot_id, cider_w, bleu_w, out);
   });
 }
 

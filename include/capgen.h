@@ -151,6 +151,18 @@ int capgen_rl_sample(capgen_t* h, const void* feats, int feats_dtype, const floa
 int capgen_rl_finish(capgen_t* h, const float* scores, float structure_loss_weight, float* loss_out, int train,
                      void* stream);
 
+/* Host rewards for self-critical training, natively (StructureCriterion.get_scores,
+ * loss.py:154-181, as restated by capgen/scst.py): out[b] = cider_w * CIDEr-D(sample_b | target_b)
+ * + bleu_w * BLEU-4(sample_b | target_b), CIDEr-D with document frequencies from the B targets
+ * (coco-caption 'corpus' mode, sigma 6, x10), per-sentence BLEU-4 with coco-caption smoothing.
+ * target / sample: host int64 [B][L] token ids (row strides target_ld / sample_ld), read as
+ * decode_captions does (core/utils.py:67-103): <START> at t = 0 skipped, <END> ends the sentence
+ * as the token dot_id ("."; pass -1 when the vocabulary has no "." word), <NULL> dropped.
+ * Pure host code: no device, no handle. */
+int capgen_scst_rewards(const int64_t* target, int64_t target_ld, const int64_t* sample, int64_t sample_ld, int B,
+                        int L, int start_id, int end_id, int null_id, int64_t dot_id, double cider_w, double bleu_w,
+                        double* out);
+
 /* Test hook: one masked multi-head attention forward (+ backward when dout != NULL) on packed
  * [B, L, H*dk] tensors (row stride H*dk), dtype 0 = f32, 1 = bf16 (the kernels the engine uses
  * for modules.py:16-27 ScaledDotProductAttention).  key_valid: optional [B][Lk] bytes (0 =

@@ -44,3 +44,25 @@ def test_reward_scorer_weights_and_entropy():
     bleu = np.array(Bleu(4).compute_score({0: ["a man ."], 1: ["a dog ."]}, {0: ["a man ."], 1: ["a horse ."]})[1][3])
     np.testing.assert_allclose(r, 0.5 * cider + 2.0 * bleu)
     np.testing.assert_allclose(sc.total(r, [1.0, 2.0]), r + 0.25 * np.array([1.0, 2.0]))
+
+
+def test_native_rewards_equal_python_restatement():
+    """libcapgen's host scorer (token ids, csrc/scst_host.cpp) equals the Python CiderD/Bleu
+    restatement on decoded strings: random samples with <END>/<NULL>/<START> anywhere, a small
+    vocabulary (many shared n-grams), with and without a "." word in the vocabulary."""
+    rng = np.random.default_rng(7)
+    for with_dot in (False, True):
+        words = ["<NULL>", "<START>", "<END>"] + [f"w{i}" for i in range(20)] + (["."] if with_dot else [])
+        idx = dict(enumerate(words))
+        for B, L in ((64, 19), (5, 3), (1, 6)):
+            target = rng.integers(3, len(words), size=(B, L))
+            sample = rng.integers(0, len(words), size=(B, L))
+            for b in range(B):  # end the references at a random length, pad after
+                e = rng.integers(1, L + 1)
+                if e < L:
+                    target[b, e] = 2
+                    target[b, e + 1:] = 0
+            py = RewardScorer(idx, cider_reward_weight=1.0, bleu_reward_weight=1.0, native=False)
+            nat = RewardScorer(idx, cider_reward_weight=1.0, bleu_reward_weight=1.0)
+            assert nat.native and not py.native
+            np.testing.assert_allclose(nat.scores(target, sample), py.scores(target, sample), rtol=1e-9, atol=1e-12)
