@@ -1391,6 +1391,8 @@ int capgen_create(const capgen_config* cfg, int device, capgen_t** out) {
     h->n_small = h->L.total - h->L.enc_lng;
     CAPGEN_HIP(hipMalloc(&h->gstripe, (size_t)capgen_engine::NSTRIPE * h->n_small * sizeof(float)));
     CAPGEN_HIP(hipHostMalloc(&h->count_host, 64, hipHostMallocDefault));
+    // the null-stream memsets above are not ordered before the engine's non-blocking streams
+    CAPGEN_HIP(hipDeviceSynchronize());
     *out = h.release();
   });
 }
@@ -1453,6 +1455,7 @@ int capgen_set_adam_state(capgen_t* h, int64_t step, const float* m, const float
     else CAPGEN_HIP(hipMemset(h->am, 0, n * 4));
     if (v) CAPGEN_HIP(hipMemcpy(h->av, v, n * 4, hipMemcpyHostToDevice));
     else CAPGEN_HIP(hipMemset(h->av, 0, n * 4));
+    CAPGEN_HIP(hipDeviceSynchronize());
   });
 }
 

@@ -376,15 +376,21 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmArgs g, int
 // Grouped launch: up to kMaxGroup independent GEMMs of one layout (e.g. every weight gradient
 // of a transformer block), each with its own M/N/pointers, tiles laid out problem after
 // problem; one launch instead of one per weight, and a grid that fills the chip.
+// G < nblk: a capped grid, each workgroup looping over the tiles b, b + G, ... (G % 8 == 0
+// keeps every iteration on the workgroup's XCD).
 template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int STAGES>
-__global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_grouped_kernel(GemmGroup gg, int nblk, const void* zero) {
+__global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_grouped_kernel(GemmGroup gg, int nblk, int G,
+                                                                        const void* zero) {
   __shared__ __attribute__((aligned(1024))) char smem[TileCfg<TA, TB, BM, BN, WM, WN, STAGES>::SMEM];
-  const int slot = xcd_slot(blockIdx.x, nblk);
-  int q = 0;
-  while (q + 1 < gg.n && slot >= gg.start[q + 1]) ++q;
-  const int tile = slot - gg.start[q];
-  const int mt = tile / gg.tiles_n[q], nt = tile % gg.tiles_n[q];
-  gemm_tile<TO, TA, TB, BM, BN, WM, WN, STAGES>(gg.p[q], mt, nt, tile, 0, 1, zero, nullptr, nullptr, smem);
+  for (int b = blockIdx.x; b < nblk; b += G) {
+    if (b != (int)blockIdx.x) __syncthreads();  // the previous tile's LDS reads are done
+    const int slot = xcd_slot(b, nblk);
+    int q = 0;
+    while (q + 1 < gg.n && slot >= gg.start[q + 1]) ++q;
+    const int tile = slot - gg.start[q];
+    const int mt = tile / gg.tiles_n[q], nt = tile % gg.tiles_n[q];
+    gemm_tile<TO, TA, TB, BM, BN, WM, WN, STAGES>(gg.p[q], mt, nt, tile, 0, 1, zero, nullptr, nullptr, smem);
+  }
 }
 
 // split-K f32 workspaces, one per stream (GEMMs on different streams may run concurrently)
@@ -403,13 +409,16 @@ void ensure_ws(hipStream_t s, size_t bytes) {
   Workspace& w = g_ws[s];
   if (!w.cnt) {
     CAPGEN_HIP(hipMalloc(&w.cnt, kMaxTiles * sizeof(int)));
-    CAPGEN_HIP(hipMemset(w.cnt, 0, kMaxTiles * sizeof(int)));
+    // on the stream itself: a null-stream hipMemset is not ordered before work on the
+    // (non-blocking) engine streams, and a split-K launch reading stale tickets combines the
+    // wrong slices (seen as a rare train_step vs forward/backward mismatch)
+    CAPGEN_HIP(hipMemsetAsync(w.cnt, 0, kMaxTiles * sizeof(int), s));
   }
   if (w.bytes >= bytes) return;
-  if (w.p) {
-    CAPGEN_HIP(hipStreamSynchronize(s));
-    CAPGEN_HIP(hipFree(w.p));
-  }
+  // a grown workspace retires the old one without freeing it: a graph captured earlier on
+  // this stream (the replayed forward) still holds its address
+  static std::vector<float*> retired;
+  if (w.p) retired.push_back(w.p);
   CAPGEN_HIP(hipMalloc(&w.p, bytes));
   w.bytes = bytes;
 }
@@ -620,7 +629,20 @@ static void launch_group_cfg(const GemmArgs* ps, int n, hipStream_t s) {
     tot += tn * tm;
   }
   gg.start[n] = tot;
-  gemm_bf16_grouped_kernel<TO, TA, TB, BM, BN, WM, WN, ST><<<tot, 64 * WM * WN, 0, s>>>(gg, tot, g_zero_page[dev]);
+  // the grouped (weight-gradient) grid is capped at one workgroup per CU, each looping over its
+  // tiles: the side-stream dW work then leaves room on every CU for the critical stream's
+  // latency-bound kernels (step 3.44-3.47 vs 3.54 ms uncapped; 64 workgroups: 3.75 ms, the dW
+  // work becomes critical).  CAPGEN_DW_GRID overrides (0 = uncapped).
+  static const int cap = [] {
+    const char* e = std::getenv("CAPGEN_DW_GRID");
+    if (e) return std::atoi(e) / 8 * 8;
+    int n = 0, dev = 0;
+    CAPGEN_HIP(hipGetDevice(&dev));
+    CAPGEN_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    return std::max(8, n / 8 * 8);
+  }();
+  const int G = cap > 0 ? std::min(tot, cap) : tot;
+  gemm_bf16_grouped_kernel<TO, TA, TB, BM, BN, WM, WN, ST><<<G, 64 * WM * WN, 0, s>>>(gg, tot, G, g_zero_page[dev]);
 }
 
 // the variants worth a grouped launch (many tiles already: no split-K)
@@ -726,6 +748,7 @@ void gemm_init() {
   if (!g_zero_page[dev]) {
     CAPGEN_HIP(hipMalloc(&g_zero_page[dev], 4096));
     CAPGEN_HIP(hipMemset(g_zero_page[dev], 0, 4096));
+    CAPGEN_HIP(hipDeviceSynchronize());  // ordered before work on non-blocking streams
   }
 }
 
