@@ -64,7 +64,7 @@ class CapgenConfig:
 
     def check_supported(self) -> None:
         """Raise NotImplementedError for reference variants the engine does not build."""
-        bad = [n for n in ("move_first_image_feature", "split_position", "split_image_objects")
+        bad = [n for n in ("move_first_image_feature", "split_image_objects")
                if getattr(self, n)]
         if bad:
             raise NotImplementedError(f"capgen: variant flags not supported: {bad}")

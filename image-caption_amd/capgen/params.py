@@ -33,8 +33,12 @@ def _ffn_specs(prefix, d, f):
 def reference_param_specs(cfg: CapgenConfig):
     """[(name, shape)] of trainable parameters, reference registration order."""
     d, f = cfg.encode_input_size, cfg.encode_hidden_size
-    specs = [("encoder.position_embedding.weight", (d, cfg.encode_dim_positions)),
-             ("encoder.feature_embedding.weight", (d, cfg.encode_dim_features)),
+    P = cfg.encode_dim_positions
+    if cfg.split_position:  # model.py:231-233: object_embedding registered first
+        specs = [("encoder.object_embedding.weight", (d, P - 4)), ("encoder.position_embedding.weight", (d, 4))]
+    else:
+        specs = [("encoder.position_embedding.weight", (d, P))]
+    specs += [("encoder.feature_embedding.weight", (d, cfg.encode_dim_features)),
              ("encoder.norm.weight", (d,)), ("encoder.norm.bias", (d,))]
     for i in range(cfg.encode_num_blocks):
         specs += _mha_specs(f"encoder.encoder.{i}.multihead_attention", d)

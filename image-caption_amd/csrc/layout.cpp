@@ -12,6 +12,7 @@ void validate_config(const capgen_config& c) {
   require(c.max_length >= 2 && c.max_length - 1 <= 64, "config: max_length must be in [2, 65]");
   require(c.dim_features > 0 && c.dim_features % 8 == 0, "config: dim_features must be a multiple of 8");
   require(c.dim_positions > 0, "config: dim_positions must be positive");
+  require(!c.split_position || c.dim_positions > 4, "config: split_position needs dim_positions > 4");
   require(c.enc_d == c.dec_d, "config: encoder and decoder widths must match");
   require(c.enc_d % 64 == 0 && c.enc_d <= 1024 && ((c.enc_d / 64) & (c.enc_d / 64 - 1)) == 0,
           "config: model width must be 64 * {1,2,4,8,16}");
@@ -127,7 +128,15 @@ Layout make_layout(const capgen_config& c) {
   L.total = (b.cur + 63) / 64 * 64;
 
   // ---- reference names, registration order (model.py:44-69; modules.py:42-62, 100-107) ----
-  b.name("encoder.position_embedding.weight", 2, d, L.P, L.enc_emb_W + L.F, L.Kp);
+  // split_position (model.py:231-233, 297-303): feats.W_f^T + pos[:, :4].W_p^T + pos[:, 4:].W_o^T is
+  // the one packed product over [feats | pos]; only the names of the position columns change
+  // (object_embedding registered first, model.py:231-233)
+  if (c.split_position) {
+    b.name("encoder.object_embedding.weight", 2, d, L.P - 4, L.enc_emb_W + L.F + 4, L.Kp);
+    b.name("encoder.position_embedding.weight", 2, d, 4, L.enc_emb_W + L.F, L.Kp);
+  } else {
+    b.name("encoder.position_embedding.weight", 2, d, L.P, L.enc_emb_W + L.F, L.Kp);
+  }
   b.name("encoder.feature_embedding.weight", 2, d, L.F, L.enc_emb_W, L.Kp);
   b.vec("encoder.norm.weight", d, L.enc_lng);
   b.vec("encoder.norm.bias", d, L.enc_lnb);

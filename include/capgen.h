@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define CAPGEN_ABI_VERSION 1
+#define CAPGEN_ABI_VERSION 2
 
 typedef struct capgen_engine capgen_t;
 
@@ -43,6 +43,11 @@ typedef struct capgen_config {
   int32_t pad_idx;                                     /* PAD_IDX */
   int32_t encode_mask;                                 /* ENCODE_MASK (model.py:311-328) */
   int32_t focal_loss;                                  /* 'FocalLoss' in OUTPUT_NAME (model.py:73-76) */
+  int32_t split_position;                              /* SPLIT_POSITION (model.py:231-233, 297-303): the
+                                                          position Linear split into Linear(4, d) over
+                                                          the box columns and Linear(P-4, d) over the
+                                                          class columns; the same arena columns, two
+                                                          table entries (position_ / object_embedding) */
   int32_t dtype;                                       /* capgen_dtype: compute/storage of activations */
   int32_t max_batch, max_regions;                      /* workspace sizing hints */
   float lr, beta1, beta2, eps;                         /* torch.optim.Adam (models.py:111-113) */

@@ -14,6 +14,7 @@ FIXTURE_CFG = {
     "c1_encmask": (lambda: preset("C1", encode_mask=True), 1),
     "c1_focal": (lambda: preset("C1", output_name="FocalLoss_Transformer"), 2),
     "c2s": (lambda: preset("C2", num_vocab=1000), 3),
+    "c1_splitpos": (lambda: preset("C1", split_position=True), 4),
     # RL_FIXTURES (SCST, injected rewards)
     "c5_rl": (lambda: preset("C1"), 5),
     "c5_rl_pad": (lambda: preset("C1"), 6),

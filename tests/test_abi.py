@@ -60,9 +60,27 @@ def test_bad_config_raises_loudly():
     cfg = preset("C1", num_vocab=1001)
     with pytest.raises(NotImplementedError):
         _lib.param_table(cfg)
-    cfg = preset("C1", split_position=True)
+    cfg = preset("C1", split_image_objects=True)
     with pytest.raises(NotImplementedError):
         _lib.param_table(cfg)
+
+
+def test_split_position_names_the_same_columns():
+    """SPLIT_POSITION (model.py:231-233, 297-303): object_embedding [d, P-4] then
+    position_embedding [d, 4], together exactly the unsplit position columns."""
+    plain, n0 = _lib.param_table(preset("C1"))
+    split, n1 = _lib.param_table(preset("C1", split_position=True))
+    assert n0 == n1
+    t0 = {e[0]: e for e in plain}
+    t1 = {e[0]: e for e in split}
+    assert [e[0] for e in split][:2] == ["encoder.object_embedding.weight", "encoder.position_embedding.weight"]
+    _, _, rows, cols, off, stride = t0["encoder.position_embedding.weight"]
+    o = t1["encoder.object_embedding.weight"]
+    p = t1["encoder.position_embedding.weight"]
+    assert (p[2], p[3], p[4], p[5]) == (rows, 4, off, stride)
+    assert (o[2], o[3], o[4], o[5]) == (rows, cols - 4, off + 4, stride)
+    assert {k: v for k, v in t0.items() if "position_embedding" not in k} == \
+        {k: v for k, v in t1.items() if "_embedding.weight" not in k or "feature" in k or "word" in k}
 
 
 def test_engine_refuses_cpu_device():

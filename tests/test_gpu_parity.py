@@ -27,7 +27,7 @@ def _inputs(z):
     return [torch.from_numpy(z[k]).to(DEV) for k in ("feats", "pos", "caps")]
 
 
-@pytest.mark.parametrize("tag", ["c1", "c1_encmask", "c1_focal", "c2s"])
+@pytest.mark.parametrize("tag", ["c1", "c1_encmask", "c1_focal", "c2s", "c1_splitpos"])
 def test_forward_fp32_matches_golden(tag):
     cfg, seed, z = load_fixture(tag)
     e = _engine(cfg, seed)
@@ -41,7 +41,7 @@ def test_forward_fp32_matches_golden(tag):
     np.testing.assert_allclose(lg, z["logits"], atol=1e-3, rtol=0)
 
 
-@pytest.mark.parametrize("tag", ["c1", "c1_encmask", "c1_focal", "c2s"])
+@pytest.mark.parametrize("tag", ["c1", "c1_encmask", "c1_focal", "c2s", "c1_splitpos"])
 def test_backward_fp32_matches_golden(tag):
     cfg, seed, z = load_fixture(tag)
     e = _engine(cfg, seed)
