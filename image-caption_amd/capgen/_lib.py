@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcapgen.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 F32, BF16 = 0, 1
 
@@ -28,7 +28,8 @@ class capgen_config(C.Structure):
         ("dec_d", C.c_int32), ("dec_ff", C.c_int32), ("dec_blocks", C.c_int32), ("dec_heads", C.c_int32),
         ("dropout", C.c_float), ("attention_dropout", C.c_float),
         ("pad_idx", C.c_int32), ("encode_mask", C.c_int32), ("focal_loss", C.c_int32),
-        ("split_position", C.c_int32),
+        ("split_position", C.c_int32), ("split_image_objects", C.c_int32),
+        ("move_first_image_feature", C.c_int32),
         ("dtype", C.c_int32), ("max_batch", C.c_int32), ("max_regions", C.c_int32),
         ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float),
         ("seed", C.c_uint64),
@@ -122,6 +123,8 @@ def to_c_config(cfg) -> capgen_config:
     c.dropout, c.attention_dropout = cfg.dropout, cfg.attention_dropout
     c.pad_idx, c.encode_mask, c.focal_loss = cfg.pad_idx, int(cfg.encode_mask), int(cfg.focal_loss)
     c.split_position = int(cfg.split_position)
+    c.split_image_objects = int(cfg.split_image_objects)
+    c.move_first_image_feature = int(cfg.move_first_image_feature)
     c.dtype = F32 if cfg.dtype == "fp32" else BF16
     c.max_batch, c.max_regions = cfg.max_batch, cfg.max_regions
     c.lr, c.beta1, c.beta2, c.eps = cfg.learning_rate, cfg.beta1, cfg.beta2, cfg.eps

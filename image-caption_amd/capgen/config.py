@@ -64,10 +64,9 @@ class CapgenConfig:
 
     def check_supported(self) -> None:
         """Raise NotImplementedError for reference variants the engine does not build."""
-        bad = [n for n in ("move_first_image_feature", "split_image_objects")
-               if getattr(self, n)]
-        if bad:
-            raise NotImplementedError(f"capgen: variant flags not supported: {bad}")
+        if self.split_position and self.split_image_objects:
+            raise NotImplementedError("capgen: split_position with split_image_objects fails in the reference "
+                                      "itself (model.py:258-292 feeds the full position row to Linear(4, d))")
         if self.encode_input_size != self.decode_input_size:
             raise NotImplementedError("capgen: encoder and decoder widths must match "
                                       "(cross-attention K/V are projected from the encoder output)")

@@ -38,6 +38,9 @@ def reference_param_specs(cfg: CapgenConfig):
         specs = [("encoder.object_embedding.weight", (d, P - 4)), ("encoder.position_embedding.weight", (d, 4))]
     else:
         specs = [("encoder.position_embedding.weight", (d, P))]
+    if cfg.split_image_objects:  # model.py:237-244: encoder.image_encoder registered next
+        specs += _mha_specs("encoder.image_encoder.multihead_attention", d)
+        specs += _ffn_specs("encoder.image_encoder.feed_forward", d, f)
     specs += [("encoder.feature_embedding.weight", (d, cfg.encode_dim_features)),
              ("encoder.norm.weight", (d,)), ("encoder.norm.bias", (d,))]
     for i in range(cfg.encode_num_blocks):
@@ -47,6 +50,10 @@ def reference_param_specs(cfg: CapgenConfig):
     specs += [("decoder.word_embedding.weight", (cfg.num_vocab, cfg.dim_word_embedding)),
               ("decoder.word_embedding_linear.weight", (dd, cfg.dim_word_embedding)),
               ("decoder.norm.weight", (dd,)), ("decoder.norm.bias", (dd,))]
+    if cfg.move_first_image_feature:  # model.py:400-407
+        specs += [("decoder.position_wise_1.weight", (df, dd)), ("decoder.position_wise_1.bias", (df,)),
+                  ("decoder.position_wise_2.weight", (dd, df)), ("decoder.position_wise_2.bias", (dd,)),
+                  ("decoder.layer_norm.weight", (dd,)), ("decoder.layer_norm.bias", (dd,))]
     for i in range(cfg.decode_num_blocks):
         specs += _mha_specs(f"decoder.decoder.{i}.self_attention", dd)
         specs += _mha_specs(f"decoder.decoder.{i}.encode_attention", dd)

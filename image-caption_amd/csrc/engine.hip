@@ -27,6 +27,7 @@
 #include "gemm.h"
 #include "layout.h"
 #include "ops.h"
+#include "variants.h"
 #include "rl.h"
 
 using namespace capgen;
@@ -97,6 +98,15 @@ struct Acts {
     void *gAf, *gH, *gA1, *gATT1, *gQKV, *gA2, *gATT2, *gQc;
   };
   std::vector<GradBufs> genc, gdec;
+  // split_image_objects (model.py:258-292): the image block runs over 2*B*N pair rows
+  void *siY, *siEp, *siX2, *siZ, *siV, *siG0, *siG1, *siGY, *siGEp;
+  uint8_t* siValid;
+  float *siM, *siR;
+  EncAct si;
+  GradBufs gsi;
+  // move_first_image_feature (model.py:451-457): U = D + enc[:, 0], H, LN output
+  void *mfU, *mfH, *mfV, *mfOut, *mfGA, *mfGH, *mfGU;
+  float *mfM, *mfR;
 };
 
 struct GenWS {
@@ -449,6 +459,51 @@ struct capgen_engine {
       T_(gb.gQKV, Me * 3 * d);
       gb.gA2 = gb.gATT2 = gb.gQc = nullptr;
     }
+    if (L_().has_img) {  // sized 0 otherwise (the planner still hands out aligned pointers)
+      const int64_t M2 = 2 * Me;
+      T_(a.siY, Me * d);
+      T_(a.siEp, Me * d);
+      T_(a.siX2, M2 * d);
+      T_(a.siZ, M2 * d);
+      T_(a.siV, Me * d);
+      T_(a.siG0, M2 * d);
+      T_(a.siG1, M2 * d);
+      T_(a.siGY, Me * d);
+      T_(a.siGEp, Me * d);
+      p.take(a.siValid, M2);
+      p.take(a.siM, Me);
+      p.take(a.siR, Me);
+      auto& l = a.si;
+      T_(l.qkv, M2 * 3 * d);
+      p.take(l.P, (size_t)Me * L_().He * 4);
+      T_(l.att, M2 * d);
+      T_(l.v1, M2 * d);
+      p.take(l.m1, M2);
+      p.take(l.r1, M2);
+      T_(l.Y, M2 * d);
+      T_(l.H, M2 * L_().fe);
+      T_(l.v2, M2 * d);
+      p.take(l.m2, M2);
+      p.take(l.r2, M2);
+      auto& gb = a.gsi;
+      T_(gb.gAf, M2 * d);
+      T_(gb.gH, M2 * L_().fe);
+      T_(gb.gA1, M2 * d);
+      T_(gb.gATT1, M2 * d);
+      T_(gb.gQKV, M2 * 3 * d);
+      gb.gA2 = gb.gATT2 = gb.gQc = nullptr;
+    }
+    if (L_().has_mf) {
+      T_(a.mfU, Md * dd);
+      T_(a.mfH, Md * L_().fd);
+      T_(a.mfV, Md * dd);
+      T_(a.mfOut, Md * dd);
+      T_(a.mfGA, Md * dd);
+      T_(a.mfGH, Md * L_().fd);
+      T_(a.mfGU, Md * dd);
+      p.take(a.mfM, Md);
+      p.take(a.mfR, Md);
+    }
     a.gdec.resize(L_().Ld);
     for (auto& gb : a.gdec) {
       T_(gb.gAf, Md * dd);
@@ -493,6 +548,74 @@ struct capgen_engine {
   }
 
   // ------------------------------------------------------------------------------------
+  // one EncoderBlock (modules.py:146-157) over B sequences of N rows: X -> Xout.  valid != null:
+  // key-pad OR causal self-attention mask and the non-pad multiply (model.py:312-328).
+  void enc_layer_fwd(const EncLayerOff& w, EncAct& A, const void* X, void* Xout, int B, int N, const uint8_t* valid,
+                     int layer, bool drop_on, hipStream_t s) {
+    const int Me = B * N, d = L.d, He = L.He, dke = d / He;
+    const float p = cfg.dropout, pa = cfg.attention_dropout;
+    linear(X, d, w.Wqkv, d, A.qkv, 3 * d, act, Me, 3 * d, d, nullptr, 0, s);
+    AttnGeom g;
+    g.B = B, g.H = He, g.Lq = N, g.Lk = N, g.dk = dke;
+    g.q = A.qkv, g.q_ld = 3 * d, g.q_bs = (int64_t)N * 3 * d;
+    g.k = at(A.qkv, d), g.k_ld = 3 * d, g.k_bs = (int64_t)N * 3 * d;
+    g.v = at(A.qkv, 2 * d), g.v_ld = 3 * d, g.v_bs = (int64_t)N * 3 * d;
+    g.o_ld = d, g.o_bs = (int64_t)N * d;
+    if (valid) g.key_valid = valid, g.kv_bs = N, g.causal = 1;
+    g.temperature = std::sqrt((float)dke);
+    g.drop = mk_drop(pa, site(0, layer, 0), drop_on);
+    attention_fwd(g, A.att, keep_probs(g) ? A.P : nullptr, act, s);
+    LnFwd l1;
+    l1.M = Me, l1.d = d, l1.a = a.tmp, l1.drop = mk_drop(p, site(0, layer, 1), drop_on), l1.res = X;
+    l1.gamma = P(w.ln1g), l1.beta = P(w.ln1b), l1.y = A.Y, l1.v_save = A.v1, l1.mean = A.m1, l1.rstd = A.r1;
+    linear_ln(A.att, d, w.Wo, d, Me, d, d, l1, s);
+    linear(A.Y, d, w.W1, d, A.H, L.fe, act, Me, L.fe, d, P(w.b1), 1, s);
+    LnFwd l2;
+    l2.M = Me, l2.d = d, l2.a = a.tmp, l2.a_bias = P(w.b2), l2.drop = mk_drop(p, site(0, layer, 2), drop_on);
+    l2.res = A.Y, l2.gamma = P(w.ln2g), l2.beta = P(w.ln2b), l2.mask.valid = valid;
+    l2.y = Xout, l2.v_save = A.v2, l2.mean = A.m2, l2.rstd = A.r2;
+    linear_ln(A.H, L.fe, w.W2, L.fe, Me, d, L.fe, l2, s);
+  }
+  static constexpr int kImgLayer = 63;  // dropout-site layer index of encoder.image_encoder
+
+  // split_image_objects (model.py:258-292, then the shared norm :294): a.Aenc -> a.X[0]
+  void image_objects_fwd(int B, int N, bool drop_on, hipStream_t s) {
+    const int Me = B * N, d = L.d;
+    // LN([feats | pos] . W^T) per token; the pair rows only repeat rows, so embed each region once
+    LnFwd ln;
+    ln.M = Me, ln.d = d, ln.a = a.tmp, ln.gamma = P(L.enc_lng), ln.beta = P(L.enc_lnb);
+    ln.y = a.siY, ln.v_save = a.ev0, ln.mean = a.em0, ln.rstd = a.er0;
+    linear_ln(a.Aenc, L.Kp, L.enc_emb_W, L.Kp, Me, d, L.Kp, ln, s);
+    // the position embedding alone (added to the region token after the image block): the
+    // position columns [F, Kp) of the packed input and weight (zero beyond F + P)
+    linear(at(a.Aenc, L.F), L.Kp, L.enc_emb_W + L.F, L.Kp, a.siEp, d, act, Me, d, L.Kp - L.F, nullptr, 0, s);
+    pair_gather(a.siY, a.valid, B, N, d, a.siX2, a.siValid, act, s);
+    enc_layer_fwd(L.img, a.si, a.siX2, a.siZ, Me, 2, a.siValid, kImgLayer, drop_on, s);
+    pair_take_add(a.siZ, a.siEp, Me, d, a.tmp, act, s);
+    LnFwd l2;
+    l2.M = Me, l2.d = d, l2.a = a.tmp, l2.gamma = P(L.enc_lng), l2.beta = P(L.enc_lnb);
+    l2.y = a.X[0], l2.v_save = a.siV, l2.mean = a.siM, l2.rstd = a.siR;
+    layernorm_fwd(l2, act, s);
+  }
+  static constexpr int kMfLayer = 62;  // dropout-site layer index of the decoder's move-first FFN
+
+  // move_first_image_feature (model.py:451-457): y = LN(x + drop(W2 relu(W1 (x + enc[:, 0]) + b1) + b2))
+  // over the M decoder rows in x (row r -> image r / rows_per_img, or r % bmod)
+  void move_first_fwd(const void* x, const void* enc, int M, int rows_per_img, int bmod, int N, void* U, void* H,
+                      void* tmp, void* y, void* v_save, float* mean, float* rstd, bool drop_on, hipStream_t s) {
+    const int dd = L.dd;
+    add_first_region(x, enc, M, rows_per_img, bmod, N, dd, U, act, s);
+    linear(U, dd, L.mf_W1, dd, H, L.fd, act, M, L.fd, dd, P(L.mf_b1), 1, s);
+    LnFwd ln;
+    ln.M = M, ln.d = dd, ln.a = tmp, ln.a_bias = P(L.mf_b2), ln.drop = mk_drop(cfg.dropout, site(1, kMfLayer, 0), drop_on);
+    ln.res = x, ln.gamma = P(L.mf_lng), ln.beta = P(L.mf_lnb), ln.y = y, ln.v_save = v_save, ln.mean = mean;
+    ln.rstd = rstd;
+    linear_ln(H, L.fd, L.mf_W2, L.fd, M, dd, L.fd, ln, s);
+  }
+  // the decoder output the classifier reads
+  void* dec_out() const { return L.has_mf ? a.mfOut : a.D[L.Ld]; }
+
+  // ------------------------------------------------------------------------------------
   // forward (model.py:79-98).  Always keeps the activations needed by backward.
   void forward(const void* feats, DType ft, const float* pos, const int32_t* caps, int B, int N, int T,
                float* loss_out, bool drop_on, hipStream_t s) {
@@ -514,41 +637,16 @@ struct capgen_engine {
     }
 
     // ---- encoder (model.py:294-332) ----
-    {
+    if (L.has_img) {
+      image_objects_fwd(B, N, drop_on, s);
+    } else {
       LnFwd ln;
       ln.M = Me, ln.d = d, ln.a = a.tmp, ln.gamma = P(L.enc_lng), ln.beta = P(L.enc_lnb);
       ln.y = a.X[0], ln.v_save = a.ev0, ln.mean = a.em0, ln.rstd = a.er0;
       linear_ln(a.Aenc, L.Kp, L.enc_emb_W, L.Kp, Me, d, L.Kp, ln, s);
     }
-    RowMask emask{};
-    if (cfg.encode_mask) emask.valid = a.valid;
-    for (int l = 0; l < L.Le; ++l) {
-      const auto& w = L.enc[l];
-      auto& A = a.enc[l];
-      linear(a.X[l], d, w.Wqkv, d, A.qkv, 3 * d, act, Me, 3 * d, d, nullptr, 0, s);
-      AttnGeom g;
-      g.B = B, g.H = He, g.Lq = N, g.Lk = N, g.dk = dke;
-      g.q = A.qkv, g.q_ld = 3 * d, g.q_bs = (int64_t)N * 3 * d;
-      g.k = at(A.qkv, d), g.k_ld = 3 * d, g.k_bs = (int64_t)N * 3 * d;
-      g.v = at(A.qkv, 2 * d), g.v_ld = 3 * d, g.v_bs = (int64_t)N * 3 * d;
-      g.o_ld = d, g.o_bs = (int64_t)N * d;
-      if (cfg.encode_mask) {  // model.py:312-319: key-pad OR causal over regions
-        g.key_valid = a.valid, g.kv_bs = N, g.causal = 1;
-      }
-      g.temperature = std::sqrt((float)dke);
-      g.drop = mk_drop(pa, site(0, l, 0), drop_on);
-      attention_fwd(g, A.att, keep_probs(g) ? A.P : nullptr, act, s);
-      LnFwd l1;
-      l1.M = Me, l1.d = d, l1.a = a.tmp, l1.drop = mk_drop(p, site(0, l, 1), drop_on), l1.res = a.X[l];
-      l1.gamma = P(w.ln1g), l1.beta = P(w.ln1b), l1.y = A.Y, l1.v_save = A.v1, l1.mean = A.m1, l1.rstd = A.r1;
-      linear_ln(A.att, d, w.Wo, d, Me, d, d, l1, s);
-      linear(A.Y, d, w.W1, d, A.H, L.fe, act, Me, L.fe, d, P(w.b1), 1, s);
-      LnFwd l2;
-      l2.M = Me, l2.d = d, l2.a = a.tmp, l2.a_bias = P(w.b2), l2.drop = mk_drop(p, site(0, l, 2), drop_on);
-      l2.res = A.Y, l2.gamma = P(w.ln2g), l2.beta = P(w.ln2b), l2.mask = emask;
-      l2.y = a.X[l + 1], l2.v_save = A.v2, l2.mean = A.m2, l2.rstd = A.r2;
-      linear_ln(A.H, L.fe, w.W2, L.fe, Me, d, L.fe, l2, s);
-    }
+    for (int l = 0; l < L.Le; ++l)
+      enc_layer_fwd(L.enc[l], a.enc[l], a.X[l], a.X[l + 1], B, N, cfg.encode_mask ? a.valid : nullptr, l, drop_on, s);
     // cross-attention K/V of every decoder block in one GEMM over the encoder output
     linear(a.X[L.Le], d, L.Wkv_all, d, a.KV, (int64_t)L.Ld * 2 * dd, act, Me, L.Ld * 2 * dd, d, nullptr, 0, s);
 
@@ -606,8 +704,10 @@ struct capgen_engine {
       l3.y = a.D[l + 1], l3.v_save = A.vf, l3.mean = A.mf, l3.rstd = A.rf;
       linear_ln(A.H, L.fd, w.W2, L.fd, Md, dd, L.fd, l3, s);
     }
+    if (L.has_mf)
+      move_first_fwd(a.D[L.Ld], a.X[L.Le], Md, Lq, 0, N, a.mfU, a.mfH, a.tmp, a.mfOut, a.mfV, a.mfM, a.mfR, drop_on, s);
     // ---- classifier + CE (model.py:93-96) ----
-    linear(a.D[L.Ld], dd, L.Wc, dd, a.logits, L.V, DType::F32, Md, L.V, dd, P(L.bc), 0, s);
+    linear(dec_out(), dd, L.Wc, dd, a.logits, L.V, DType::F32, Md, L.V, dd, P(L.bc), 0, s);
     cross_entropy_rows(a.logits, a.tgt, Md, L.V, cfg.pad_idx, a.loss_row, a.dlogits, act, s);
     loss_finalize(a.loss_row, Md, a.count, cfg.focal_loss, loss_out ? loss_out : a.loss, a.grad_scale, s);
   }
@@ -730,6 +830,66 @@ struct capgen_engine {
   int64_t enc_end(int l) const { return l + 1 < L.Le ? L.enc[l + 1].Wqkv : L.Wel; }
   int64_t dec_end(int l) const { return l + 1 < L.Ld ? L.dec[l + 1].Wqkv : L.Wkv_all; }
 
+  // backward of enc_layer_fwd: gO = grad wrt Xout on entry, grad wrt X on exit; gR scratch
+  void enc_layer_bwd(const EncLayerOff& w, EncAct& A, Acts::GradBufs& gb, const void* X, int B, int N,
+                     const uint8_t* valid, int layer, bool on, void* gO, void* gR, hipStream_t s) {
+    const int Me = B * N, d = L.d, He = L.He, dke = d / He;
+    const float p = cfg.dropout, pa = cfg.attention_dropout;
+    RowMask mask{};
+    mask.valid = valid;
+    const LnBwd lffn = lnb_desc(Me, d, gO, A.v2, A.m2, A.r2, w.ln2g, w.ln2b, w.b2, mask, mk_drop(p, site(0, layer, 2), on),
+                                gR, gb.gAf);
+    const LnBwd lmha = lnb_desc(Me, d, gR, A.v1, A.m1, A.r1, w.ln1g, w.ln1b, -1, RowMask{},
+                                mk_drop(p, site(0, layer, 1), on), gO, gb.gA1);
+    ffn_bwd(Me, d, L.fe, lffn, A.Y, A.H, w.W1, w.b1, w.W2, gb.gH, s);  // gR = grad wrt Y
+    mha_out_bwd(Me, d, lmha, A.att, w.Wo, gb.gATT1, s);
+    AttnGeom g;
+    g.B = B, g.H = He, g.Lq = N, g.Lk = N, g.dk = dke;
+    g.q = A.qkv, g.q_ld = 3 * d, g.q_bs = (int64_t)N * 3 * d;
+    g.k = at(A.qkv, d), g.k_ld = 3 * d, g.k_bs = (int64_t)N * 3 * d;
+    g.v = at(A.qkv, 2 * d), g.v_ld = 3 * d, g.v_bs = (int64_t)N * 3 * d;
+    g.o_ld = d, g.o_bs = (int64_t)N * d;
+    if (valid) g.key_valid = valid, g.kv_bs = N, g.causal = 1;
+    g.temperature = std::sqrt((float)dke);
+    g.drop = mk_drop(pa, site(0, layer, 0), on);
+    attention_bwd(g, A.P, gb.gATT1, gb.gQKV, at(gb.gQKV, d), at(gb.gQKV, 2 * d), act, s);
+    dw_side(gb.gQKV, 3 * d, X, d, w.Wqkv, d, Me, 3 * d, d, nullptr, s);
+    linear_dx(gb.gQKV, 3 * d, w.Wqkv, d, gO, d, Me, 3 * d, d, 1, nullptr, nullptr, s);  // gO = grad wrt X
+  }
+
+  // backward of image_objects_fwd: gX0 = grad wrt a.X[0] -> embedding weight gradient
+  void image_objects_bwd(const void* gX0, int B, int N, bool on, hipStream_t s) {
+    const int Me = B * N, d = L.d;
+    // second norm: grad wrt Z[2r+1] + Ep[r] (no residual, no dropout)
+    layernorm_bwd(lnb_desc(Me, d, gX0, a.siV, a.siM, a.siR, L.enc_lng, L.enc_lnb, -1, RowMask{}, Drop{}, nullptr,
+                           a.siGEp),
+                  act, s);
+    pair_scatter(a.siGEp, Me, d, a.siG0, act, s);  // only the region token's output is kept
+    enc_layer_bwd(L.img, a.si, a.gsi, a.siX2, Me, 2, a.siValid, kImgLayer, on, a.siG0, a.siG1, s);
+    pair_reduce(a.siG0, B, N, d, a.siGY, act, s);  // image-row tokens fold back onto region 0
+    layernorm_bwd(lnb_desc(Me, d, a.siGY, a.ev0, a.em0, a.er0, L.enc_lng, L.enc_lnb, -1, RowMask{}, Drop{}, nullptr,
+                           a.gAe),
+                  act, s);
+    // feature columns see the first embedding only; position columns both (+ Ep after the block)
+    linear_dw(a.gAe, d, a.Aenc, L.Kp, L.enc_emb_W, L.Kp, Me, d, L.F, nullptr, s);
+    add_inplace(a.siGEp, a.gAe, (int64_t)Me * d, act, s);
+    linear_dw(a.siGEp, d, at(a.Aenc, L.F), L.Kp, L.enc_emb_W + L.F, L.Kp, Me, d, L.Kp - L.F, nullptr, s);
+  }
+
+  // backward of move_first_fwd at the training shape (dy = a.gOut): a.gRes = grad wrt D[Ld]
+  // (residual + U), a.mfGU = grad wrt U
+  void move_first_bwd(int Md, bool on, hipStream_t s) {
+    const int dd = L.dd, fd = L.fd;
+    const LnBwd lb = lnb_desc(Md, dd, a.gOut, a.mfV, a.mfM, a.mfR, L.mf_lng, L.mf_lnb, L.mf_b2, RowMask{},
+                              mk_drop(cfg.dropout, site(1, kMfLayer, 0), on), a.gRes, a.mfGA);
+    layernorm_bwd(lb, act, s);
+    dw_side(a.mfGA, dd, a.mfH, fd, L.mf_W2, fd, Md, dd, fd, nullptr, s);
+    linear_dx(a.mfGA, dd, L.mf_W2, fd, a.mfGH, fd, Md, dd, fd, 0, a.mfH, nullptr, s, GS(L.mf_b1));
+    dw_side(a.mfGH, fd, a.mfU, dd, L.mf_W1, dd, Md, fd, dd, nullptr, s);
+    linear_dx(a.mfGH, fd, L.mf_W1, dd, a.mfGU, dd, Md, fd, dd, 0, nullptr, nullptr, s);
+    add_inplace(a.gRes, a.mfGU, (int64_t)Md * dd, act, s);
+  }
+
   // step_params: bucketed all-reduce + Adam (see bucket()); otherwise gradients only
   void backward(hipStream_t s, bool step_params = false) {
     bstep = step_params;
@@ -745,8 +905,6 @@ struct capgen_engine {
 
     RowMask dmask{};
     dmask.ids = a.ids, dmask.pad_idx = cfg.pad_idx;
-    RowMask emask{};
-    if (cfg.encode_mask) emask.valid = a.valid;
     // the LayerNorm backward of every block (model.py:86-90, 114-120 restated backward)
     auto dec_ffn_lb = [&](int l, const void* dy, void* dres) {
       const auto& A = a.dec[l];
@@ -769,18 +927,6 @@ struct capgen_engine {
     auto dec_emb_lb = [&](const void* dy) {  // LN(E.Wel^T + PE) (model.py:432-436): no residual, no dropout
       return lnb_desc(Md, dd, dy, a.dv0, a.dm0, a.dr0, L.dec_lng, L.dec_lnb, -1, RowMask{}, Drop{}, nullptr, a.gAd);
     };
-    auto enc_ffn_lb = [&](int l, const void* dy, void* dres) {
-      const auto& A = a.enc[l];
-      const auto& w = L.enc[l];
-      return lnb_desc(Me, d, dy, A.v2, A.m2, A.r2, w.ln2g, w.ln2b, w.b2, emask, mk_drop(p, site(0, l, 2), on), dres,
-                      a.genc[l].gAf);
-    };
-    auto enc_mha_lb = [&](int l, const void* dy, void* dres) {
-      const auto& A = a.enc[l];
-      const auto& w = L.enc[l];
-      return lnb_desc(Me, d, dy, A.v1, A.m1, A.r1, w.ln1g, w.ln1b, -1, RowMask{}, mk_drop(p, site(0, l, 1), on), dres,
-                      a.genc[l].gA1);
-    };
     auto enc_emb_lb = [&](const void* dy) {
       return lnb_desc(Me, d, dy, a.ev0, a.em0, a.er0, L.enc_lng, L.enc_lnb, -1, RowMask{}, Drop{}, nullptr, a.gAe);
     };
@@ -788,13 +934,17 @@ struct capgen_engine {
     // classifier: dlogits are unscaled (softmax - onehot); grad_scale folds 1/count (+focal)
     fork(s);
     column_sum(a.dlogits, Md, L.V, L.V, 1.f, a.grad_scale, GS(L.bc), act, es2, NSTRIPE, n_small);
-    dw_side(a.dlogits, L.V, a.D[L.Ld], dd, L.Wc, dd, Md, L.V, dd, a.grad_scale, s);
+    dw_side(a.dlogits, L.V, dec_out(), dd, L.Wc, dd, Md, L.V, dd, a.grad_scale, s);
     linear_dx(a.dlogits, L.V, L.Wc, dd, a.gOut, dd, Md, L.V, dd, 0, nullptr, a.grad_scale, s);
     bucket(L.Wc, L.n_dense - L.Wc, s);  // flushed after the dX GEMM above: it reads Wc
 
     const int64_t kvld = (int64_t)L.Ld * 2 * dd;
     void* gO = a.gOut;
     void* gR = a.gRes;
+    if (L.has_mf) {  // gRes = grad wrt D[Ld]; a.mfGU = grad wrt U (its encoder part is added below)
+      move_first_bwd(Md, on, s);
+      std::swap(gO, gR);
+    }
     for (int l = L.Ld - 1; l >= 0; --l) {
       const auto& w = L.dec[l];
       auto& A = a.dec[l];
@@ -851,6 +1001,7 @@ struct capgen_engine {
     gO = eO;
     gR = a.tmp;
     linear_dx(a.gKV, kvld, L.Wkv_all, d, gO, d, Me, L.Ld * 2 * dd, d, 0, nullptr, nullptr, s);
+    if (L.has_mf) first_region_grad(a.mfGU, B, Lq, N, d, gO, act, s);  // enc[:, 0] of U = D + enc[:, 0]
     dw_side(a.gKV, kvld, a.X[L.Le], d, L.Wkv_all, d, Me, L.Ld * 2 * dd, d, nullptr, s);
     // the decoder-embedding branch (es2) has been issued: every decoder-side gradient is final
     // the flush of the first bucket follows the dX GEMM above (it reads Wkv_all); es2 then holds
@@ -861,36 +1012,26 @@ struct capgen_engine {
     bucket(L.dec_lng, L.total - L.dec_lng, s, false);     // decoder LN / biases, classifier bias
     for (int l = L.Le - 1; l >= 0; --l) {
       const auto& w = L.enc[l];
-      auto& A = a.enc[l];
-      auto& gb = a.genc[l];
-      const LnBwd lffn = enc_ffn_lb(l, gO, gR), lmha = enc_mha_lb(l, gR, gO);
-      ffn_bwd(Me, d, L.fe, lffn, A.Y, A.H, w.W1, w.b1, w.W2, gb.gH, s);  // gR = grad wrt Y
-      mha_out_bwd(Me, d, lmha, A.att, w.Wo, gb.gATT1, s);
-      AttnGeom g;
-      g.B = B, g.H = He, g.Lq = N, g.Lk = N, g.dk = dke;
-      g.q = A.qkv, g.q_ld = 3 * d, g.q_bs = (int64_t)N * 3 * d;
-      g.k = at(A.qkv, d), g.k_ld = 3 * d, g.k_bs = (int64_t)N * 3 * d;
-      g.v = at(A.qkv, 2 * d), g.v_ld = 3 * d, g.v_bs = (int64_t)N * 3 * d;
-      g.o_ld = d, g.o_bs = (int64_t)N * d;
-      if (cfg.encode_mask) g.key_valid = a.valid, g.kv_bs = N, g.causal = 1;
-      g.temperature = std::sqrt((float)dke);
-      g.drop = mk_drop(pa, site(0, l, 0), on);
-      attention_bwd(g, A.P, gb.gATT1, gb.gQKV, at(gb.gQKV, d), at(gb.gQKV, 2 * d), act, s);
-      dw_side(gb.gQKV, 3 * d, a.X[l], d, w.Wqkv, d, Me, 3 * d, d, nullptr, s);
-      linear_dx(gb.gQKV, 3 * d, w.Wqkv, d, gO, d, Me, 3 * d, d, 1, nullptr, nullptr, s);  // gO = grad wrt X_l
+      enc_layer_bwd(w, a.enc[l], a.genc[l], a.X[l], B, N, cfg.encode_mask ? a.valid : nullptr, l, on, gO, gR, s);
       bucket(w.Wqkv, enc_end(l) - w.Wqkv, s);
     }
     // the tail of the step's dependency chain: the encoder-embedding LayerNorm backward and
     // weight gradient, then its Adam, which the next forward's first GEMM needs -- on the
     // critical stream, so it does not queue behind the weight-gradient groups still on es2
     // (a single GEMM: the plain launch with its autotuned split-K, K = B*N = 2304 deep)
-    layernorm_bwd(enc_emb_lb(gO), act, s);
-    linear_dw(a.gAe, d, a.Aenc, L.Kp, L.enc_emb_W, L.Kp, Me, d, L.Kp, nullptr, s);
+    if (L.has_img) {
+      image_objects_bwd(gO, B, N, on, s);
+      flush(s);  // the image block's weight gradients share the embedding bucket
+    } else {
+      layernorm_bwd(enc_emb_lb(gO), act, s);
+      linear_dw(a.gAe, d, a.Aenc, L.Kp, L.enc_emb_W, L.Kp, Me, d, L.Kp, nullptr, s);
+    }
     // every encoder LayerNorm/bias partial was accumulated on s; in step mode the fold and the
     // last two buckets (feature/position embedding, encoder LN / biases) run on the bucket
     // stream behind ONE event (each event record costs the critical stream ~5 us)
     const hipStream_t tail = bstep ? ec : s;
     if (bstep) dep(s, ec, ev_b1);
+    if (bstep && L.has_img) dep(es2, ec, ev_b2);
     stripe_reduce(GS(L.enc_lng), NSTRIPE, n_small, L.dec_lng - L.enc_lng, G(L.enc_lng), 0, tail);
     if (bstep) {
       bucket_update(0, L.enc[0].Wqkv);                   // feature/position embedding
@@ -1060,10 +1201,14 @@ struct capgen_engine {
     const int Me = B * N, d = L.d, He = L.He, dke = d / He;
     ensure_acts(B, N, 2);
     pack_encoder_input(feats, ft, pos, Me, L.F, L.P, L.Kp, a.Aenc, act, a.valid, s);
-    linear(a.Aenc, L.Kp, L.enc_emb_W, L.Kp, a.tmp, d, act, Me, d, L.Kp, nullptr, 0, s);
-    LnFwd ln;
-    ln.M = Me, ln.d = d, ln.a = a.tmp, ln.gamma = P(L.enc_lng), ln.beta = P(L.enc_lnb), ln.y = a.X[0];
-    layernorm_fwd(ln, act, s);
+    if (L.has_img) {
+      image_objects_fwd(B, N, false, s);
+    } else {
+      linear(a.Aenc, L.Kp, L.enc_emb_W, L.Kp, a.tmp, d, act, Me, d, L.Kp, nullptr, 0, s);
+      LnFwd ln;
+      ln.M = Me, ln.d = d, ln.a = a.tmp, ln.gamma = P(L.enc_lng), ln.beta = P(L.enc_lnb), ln.y = a.X[0];
+      layernorm_fwd(ln, act, s);
+    }
     RowMask emask{};
     if (cfg.encode_mask) emask.valid = a.valid;
     for (int l = 0; l < L.Le; ++l) {
@@ -1191,7 +1336,12 @@ struct capgen_engine {
       l3.mask = rm, l3.y = g.x;
       layernorm_fwd(l3, act, s);
     }
-    linear(g.x, dd, L.Wc, dd, g.logits, L.V, DType::F32, R, L.V, dd, P(L.bc), 0, s);
+    const void* xo = g.x;
+    if (L.has_mf) {  // rows r -> image r % Bimg
+      move_first_fwd(g.x, a.X[L.Le], R, 1, Bimg, N, g.x2, g.h, g.tmp, g.x1, nullptr, nullptr, nullptr, false, s);
+      xo = g.x1;
+    }
+    linear(xo, dd, L.Wc, dd, g.logits, L.V, DType::F32, R, L.V, dd, P(L.bc), 0, s);
   }
 
   void greedy(const void* feats, DType ft, const float* pos, int B, int N, int64_t* ids_out, float* attn_out,

@@ -13,6 +13,11 @@ void validate_config(const capgen_config& c) {
   require(c.dim_features > 0 && c.dim_features % 8 == 0, "config: dim_features must be a multiple of 8");
   require(c.dim_positions > 0, "config: dim_positions must be positive");
   require(!c.split_position || c.dim_positions > 4, "config: split_position needs dim_positions > 4");
+  // model.py:258-292 applies position_embedding to the full position row, which a split
+  // Linear(4, d) cannot take: the reference itself fails on this combination
+  require(!(c.split_position && c.split_image_objects), "config: split_position and split_image_objects exclude "
+          "each other");
+  require(!c.split_image_objects || c.enc_blocks >= 1, "config: split_image_objects needs >= 1 encoder block");
   require(c.enc_d == c.dec_d, "config: encoder and decoder widths must match");
   require(c.enc_d % 64 == 0 && c.enc_d <= 1024 && ((c.enc_d / 64) & (c.enc_d / 64 - 1)) == 0,
           "config: model width must be 64 * {1,2,4,8,16}");
@@ -78,6 +83,13 @@ Layout make_layout(const capgen_config& c) {
 
   // ---- dense region (GEMM weights) ----
   L.enc_emb_W = b.take(d * L.Kp);
+  L.has_img = c.split_image_objects != 0;
+  if (L.has_img) {
+    L.img.Wqkv = b.take(3 * d * d);
+    L.img.Wo = b.take(d * d);
+    L.img.W1 = b.take((int64_t)L.fe * d);
+    L.img.W2 = b.take(d * L.fe);
+  }
   L.enc.resize(L.Le);
   for (auto& e : L.enc) {
     e.Wqkv = b.take(3 * d * d);
@@ -96,6 +108,11 @@ Layout make_layout(const capgen_config& c) {
     e.W2 = b.take(dd * L.fd);
   }
   L.Wkv_all = b.take((int64_t)L.Ld * 2 * dd * d);
+  L.has_mf = c.move_first_image_feature != 0;
+  if (L.has_mf) {
+    L.mf_W1 = b.take((int64_t)L.fd * dd);
+    L.mf_W2 = b.take(dd * L.fd);
+  }
   L.Wc = b.take((int64_t)L.V * dd);
   L.n_dense = (b.cur + 63) / 64 * 64;
   b.cur = L.n_dense;
@@ -104,6 +121,15 @@ Layout make_layout(const capgen_config& c) {
   L.emb = b.take((int64_t)L.V * L.dwe);
   L.enc_lng = b.take(d);
   L.enc_lnb = b.take(d);
+  if (L.has_img) {
+    auto& e = L.img;
+    e.ln1g = b.take(d);
+    e.ln1b = b.take(d);
+    e.b1 = b.take(L.fe);
+    e.b2 = b.take(d);
+    e.ln2g = b.take(d);
+    e.ln2b = b.take(d);
+  }
   for (auto& e : L.enc) {
     e.ln1g = b.take(d);
     e.ln1b = b.take(d);
@@ -114,6 +140,12 @@ Layout make_layout(const capgen_config& c) {
   }
   L.dec_lng = b.take(dd);
   L.dec_lnb = b.take(dd);
+  if (L.has_mf) {
+    L.mf_b1 = b.take(L.fd);
+    L.mf_b2 = b.take(dd);
+    L.mf_lng = b.take(dd);
+    L.mf_lnb = b.take(dd);
+  }
   for (auto& e : L.dec) {
     e.lsg = b.take(dd);
     e.lsb = b.take(dd);
@@ -137,12 +169,7 @@ Layout make_layout(const capgen_config& c) {
   } else {
     b.name("encoder.position_embedding.weight", 2, d, L.P, L.enc_emb_W + L.F, L.Kp);
   }
-  b.name("encoder.feature_embedding.weight", 2, d, L.F, L.enc_emb_W, L.Kp);
-  b.vec("encoder.norm.weight", d, L.enc_lng);
-  b.vec("encoder.norm.bias", d, L.enc_lnb);
-  for (int i = 0; i < L.Le; ++i) {
-    const auto& e = L.enc[i];
-    const std::string p = "encoder.encoder." + std::to_string(i) + ".";
+  auto enc_block = [&](const EncLayerOff& e, const std::string& p) {
     const std::string m = p + "multihead_attention.";
     b.mat(m + "q_linear.weight", d, d, e.Wqkv);
     b.mat(m + "k_linear.weight", d, d, e.Wqkv + d * d);
@@ -157,11 +184,24 @@ Layout make_layout(const capgen_config& c) {
     b.vec(f + "position_wise_2.bias", d, e.b2);
     b.vec(f + "layer_norm.weight", d, e.ln2g);
     b.vec(f + "layer_norm.bias", d, e.ln2b);
-  }
+  };
+  if (L.has_img) enc_block(L.img, "encoder.image_encoder.");  // model.py:237-244: after position_embedding
+  b.name("encoder.feature_embedding.weight", 2, d, L.F, L.enc_emb_W, L.Kp);
+  b.vec("encoder.norm.weight", d, L.enc_lng);
+  b.vec("encoder.norm.bias", d, L.enc_lnb);
+  for (int i = 0; i < L.Le; ++i) enc_block(L.enc[i], "encoder.encoder." + std::to_string(i) + ".");
   b.mat("decoder.word_embedding.weight", L.V, L.dwe, L.emb);
   b.mat("decoder.word_embedding_linear.weight", dd, L.dwe, L.Wel);
   b.vec("decoder.norm.weight", dd, L.dec_lng);
   b.vec("decoder.norm.bias", dd, L.dec_lnb);
+  if (L.has_mf) {  // model.py:400-407
+    b.mat("decoder.position_wise_1.weight", L.fd, dd, L.mf_W1);
+    b.vec("decoder.position_wise_1.bias", L.fd, L.mf_b1);
+    b.mat("decoder.position_wise_2.weight", dd, L.fd, L.mf_W2);
+    b.vec("decoder.position_wise_2.bias", dd, L.mf_b2);
+    b.vec("decoder.layer_norm.weight", dd, L.mf_lng);
+    b.vec("decoder.layer_norm.bias", dd, L.mf_lnb);
+  }
   for (int i = 0; i < L.Ld; ++i) {
     const auto& e = L.dec[i];
     const std::string p = "decoder.decoder." + std::to_string(i) + ".";

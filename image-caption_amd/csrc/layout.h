@@ -35,6 +35,14 @@ struct Layout {
   int64_t enc_emb_W = 0, Wel = 0, Wkv_all = 0, Wc = 0;
   std::vector<EncLayerOff> enc;
   std::vector<DecLayerOff> dec;
+  // split_image_objects: encoder.image_encoder (dense weights inside the embedding bucket
+  // [0, enc[0].Wqkv), small ones inside the encoder LN/bias region)
+  bool has_img = false;
+  EncLayerOff img{};
+  // move_first_image_feature: the decoder's trailing FFN (dense weights inside the cross-K/V
+  // bucket [Wkv_all, Wc), small ones inside the decoder LN/bias region)
+  bool has_mf = false;
+  int64_t mf_W1 = 0, mf_W2 = 0, mf_b1 = 0, mf_b2 = 0, mf_lng = 0, mf_lnb = 0;
   int64_t n_dense = 0;
   // accumulated region
   int64_t emb = 0, enc_lng = 0, enc_lnb = 0, dec_lng = 0, dec_lnb = 0, bc = 0;

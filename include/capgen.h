@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define CAPGEN_ABI_VERSION 2
+#define CAPGEN_ABI_VERSION 3
 
 typedef struct capgen_engine capgen_t;
 
@@ -48,6 +48,14 @@ typedef struct capgen_config {
                                                           the box columns and Linear(P-4, d) over the
                                                           class columns; the same arena columns, two
                                                           table entries (position_ / object_embedding) */
+  int32_t split_image_objects;                         /* SPLIT_IMAGE_OBJECTS (model.py:237-244, 258-292): an
+                                                          extra EncoderBlock (encoder.image_encoder) over
+                                                          every (image row, region) pair, causal + key-pad
+                                                          masked; its region token + the position
+                                                          embedding feed the shared encoder norm */
+  int32_t move_first_image_feature;                    /* MOVE_FIRST_IMAGE_FAETURE (model.py:400-407,
+                                                          451-457): after the last decoder block,
+                                                          LN(x + drop(FFN(x + enc_out[:, 0]))) */
   int32_t dtype;                                       /* capgen_dtype: compute/storage of activations */
   int32_t max_batch, max_regions;                      /* workspace sizing hints */
   float lr, beta1, beta2, eps;                         /* torch.optim.Adam (models.py:111-113) */

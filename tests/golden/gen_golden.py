@@ -68,7 +68,8 @@ def build(Transformer, cfg):
         dim_word_embedding=cfg.dim_word_embedding, decode_input_size=cfg.decode_input_size,
         decode_q_k_dim=cfg.decode_q_k_dim, decode_v_dim=cfg.decode_v_dim,
         decode_hidden_size=cfg.decode_hidden_size, decode_num_blocks=cfg.decode_num_blocks,
-        decode_num_heads=cfg.decode_num_heads, split_position=cfg.split_position)
+        decode_num_heads=cfg.decode_num_heads, split_position=cfg.split_position,
+        split_image_objects=cfg.split_image_objects, move_first_image_feature=cfg.move_first_image_feature)
 
 
 def make_fixture(tag, cfg, B, N, T, seed, beam_k=5, min_valid=None):
@@ -262,6 +263,8 @@ FIXTURES = {
     "c1_focal": (preset("C1", output_name="FocalLoss_Transformer"), 4, 8, 10, 2, 0, 4),
     "c2s": (preset("C2", num_vocab=1000), 2, 36, 20, 3, 5, 12),
     "c1_splitpos": (preset("C1", split_position=True), 4, 8, 10, 4, 3, 4),
+    "c1_imgobj": (preset("C1", split_image_objects=True), 4, 8, 10, 7, 3, 4),
+    "c1_movefirst": (preset("C1", move_first_image_feature=True), 4, 8, 10, 8, 3, 4),
 }
 
 

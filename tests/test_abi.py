@@ -30,9 +30,14 @@ def test_abi_version():
     assert _lib.load().capgen_abi_version() == _lib.ABI_VERSION
 
 
+VARIANTS = {"plain": {}, "imgobj": {"split_image_objects": True}, "movefirst": {"move_first_image_feature": True},
+            "both": {"split_image_objects": True, "move_first_image_feature": True}}
+
+
+@pytest.mark.parametrize("variant", sorted(VARIANTS))
 @pytest.mark.parametrize("name", ["C1", "C2"])
-def test_param_table_matches_reference_specs(name):
-    cfg = preset(name)
+def test_param_table_matches_reference_specs(name, variant):
+    cfg = preset(name, **VARIANTS[variant])
     table, total = _lib.param_table(cfg)
     specs = reference_param_specs(cfg)
     assert [t[0] for t in table] == [s[0] for s in specs]
@@ -45,7 +50,8 @@ def test_param_table_matches_reference_specs(name):
         spans.append((off, off + (rows - 1) * stride + cols, n))
         covered += rows * cols
     assert covered == num_params(cfg)
-    assert covered == (55707408 if name == "C2" else 1272808)
+    if variant == "plain":
+        assert covered == (55707408 if name == "C2" else 1272808)
     # no two tensors overlap (interleaved strided tensors checked element-wise below)
     occ = bytearray(total)
     for (n, ndim, rows, cols, off, stride) in table:
@@ -60,7 +66,7 @@ def test_bad_config_raises_loudly():
     cfg = preset("C1", num_vocab=1001)
     with pytest.raises(NotImplementedError):
         _lib.param_table(cfg)
-    cfg = preset("C1", split_image_objects=True)
+    cfg = preset("C1", split_image_objects=True, split_position=True)  # fails in the reference too
     with pytest.raises(NotImplementedError):
         _lib.param_table(cfg)
 

@@ -27,7 +27,7 @@ def _inputs(z):
     return [torch.from_numpy(z[k]).to(DEV) for k in ("feats", "pos", "caps")]
 
 
-@pytest.mark.parametrize("tag", ["c1", "c1_encmask", "c1_focal", "c2s", "c1_splitpos"])
+@pytest.mark.parametrize("tag", ["c1", "c1_encmask", "c1_focal", "c2s", "c1_splitpos", "c1_imgobj", "c1_movefirst"])
 def test_forward_fp32_matches_golden(tag):
     cfg, seed, z = load_fixture(tag)
     e = _engine(cfg, seed)
@@ -41,7 +41,7 @@ def test_forward_fp32_matches_golden(tag):
     np.testing.assert_allclose(lg, z["logits"], atol=1e-3, rtol=0)
 
 
-@pytest.mark.parametrize("tag", ["c1", "c1_encmask", "c1_focal", "c2s", "c1_splitpos"])
+@pytest.mark.parametrize("tag", ["c1", "c1_encmask", "c1_focal", "c2s", "c1_splitpos", "c1_imgobj", "c1_movefirst"])
 def test_backward_fp32_matches_golden(tag):
     cfg, seed, z = load_fixture(tag)
     e = _engine(cfg, seed)
@@ -63,7 +63,7 @@ def test_backward_fp32_matches_golden(tag):
     np.testing.assert_allclose(got, ref, atol=1e-4 + 1e-3 * np.abs(ref).max(), rtol=1e-2)
 
 
-@pytest.mark.parametrize("tag", ["c1", "c2s"])
+@pytest.mark.parametrize("tag", ["c1", "c2s", "c1_imgobj", "c1_movefirst"])
 def test_two_adam_steps_fp32(tag):
     cfg, seed, z = load_fixture(tag)
     e = _engine(cfg, seed)
@@ -86,8 +86,9 @@ def test_two_adam_steps_fp32(tag):
         assert abs(d - ref) <= 2e-2 * ref + 1e-6, (n, d, ref)
 
 
-def test_train_step_graph_equals_eager_fp32():
-    cfg, seed, z = load_fixture("c1")
+@pytest.mark.parametrize("tag", ["c1", "c1_imgobj", "c1_movefirst"])
+def test_train_step_graph_equals_eager_fp32(tag):
+    cfg, seed, z = load_fixture(tag)
     f, p, c = _inputs(z)
     a = _engine(cfg, seed, dropout=0.3)
     b = _engine(cfg, seed, dropout=0.3)
@@ -114,11 +115,13 @@ def _params_close(a, b, atol):
         torch.testing.assert_close(sa[k], sb[k], atol=atol, rtol=0, msg=k)
 
 
+@pytest.mark.parametrize("tag", ["c2s", "c1_imgobj", "c1_movefirst"])
 @pytest.mark.parametrize("graph", [False, True])
-def test_bucketed_train_step_equals_unfused_fp32(graph):
+def test_bucketed_train_step_equals_unfused_fp32(graph, tag):
     """train_step issues all-reduce + Adam per bucket on the bucket stream, overlapped with
-    backward; it must equal forward -> backward -> adam_step over the whole arena."""
-    cfg, seed, z = load_fixture("c2s")
+    backward; it must equal forward -> backward -> adam_step over the whole arena (the variant
+    flags' weights ride in the embedding / cross-K/V buckets)."""
+    cfg, seed, z = load_fixture(tag)
     f, p, c = _inputs(z)
     a = _engine(cfg, seed)
     b = _engine(cfg, seed)
@@ -156,7 +159,7 @@ def test_dp_world1_rccl_train_step_fp32(graph):
     _params_close(a, b, 1e-6)
 
 
-@pytest.mark.parametrize("tag", ["c1", "c1_encmask", "c2s"])
+@pytest.mark.parametrize("tag", ["c1", "c1_encmask", "c2s", "c1_imgobj", "c1_movefirst"])
 def test_greedy_bit_exact(tag):
     cfg, seed, z = load_fixture(tag)
     e = _engine(cfg, seed)
@@ -167,7 +170,7 @@ def test_greedy_bit_exact(tag):
     np.testing.assert_allclose(attn.cpu().numpy(), z["greedy_attn"], atol=1e-4)
 
 
-@pytest.mark.parametrize("tag", ["c1", "c1_encmask", "c2s"])
+@pytest.mark.parametrize("tag", ["c1", "c1_encmask", "c2s", "c1_imgobj", "c1_movefirst"])
 def test_beam_search_matches(tag):
     cfg, seed, z = load_fixture(tag)
     e = _engine(cfg, seed)
@@ -176,7 +179,7 @@ def test_beam_search_matches(tag):
     np.testing.assert_array_equal(ids.cpu().numpy(), z["beam_ids"])
 
 
-@pytest.mark.parametrize("tag", ["c1", "c2s"])
+@pytest.mark.parametrize("tag", ["c1", "c2s", "c1_imgobj", "c1_movefirst"])
 def test_bf16_mode_loss_close(tag):
     cfg, seed, z = load_fixture(tag)
     e = _engine(cfg, seed, dtype="bf16")

@@ -8,7 +8,7 @@ from capgen.params import fixture_state_dict, reference_param_specs, sinusoid_ta
 from golden_util import load_fixture, sample_index
 from oracle import capgen_oracle as O
 
-TAGS = ["c1", "c1_encmask", "c1_focal", "c2s", "c1_splitpos"]
+TAGS = ["c1", "c1_encmask", "c1_focal", "c2s", "c1_splitpos", "c1_imgobj", "c1_movefirst"]
 
 
 def _setup(tag):
