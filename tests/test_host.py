@@ -106,3 +106,58 @@ def test_dp_exact_mean_gloo_world2_matches_single_process():
     g = torch.cat([v.grad.reshape(-1) for v in P.values()]).numpy()
     assert abs(loss.item() - loss_dp) < 1e-5
     np.testing.assert_allclose(g_dp, g, atol=1e-6, rtol=1e-4)
+
+
+def test_train_loop_cadence_matches_main_py(tmp_path):
+    """capgen.train.train restates main.py:25-153: train_step per batch, compute_loss on the two
+    fixed eval batches every 100 steps, a greedy sample every 2500, per-epoch valid captions +
+    checkpoint.  Driven here with a recording stand-in model on the CPU (no engine calls)."""
+    import pickle
+    import numpy as np
+    import torch
+    from capgen.train import train
+
+    class Rec:
+        def __init__(self):
+            self.calls = []
+
+        def train_step_resident(self, store, idx, caps):
+            self.calls.append(("step", int(idx.shape[0])))
+
+        def compute_loss(self, object_features, position_features, target_caption):
+            self.calls.append(("loss", int(object_features.shape[0])))
+            return {"loss": torch.tensor(float(target_caption.shape[0]))}
+
+        def generate_caption(self, object_features, position_features, beam_size=None):
+            self.calls.append(("gen", int(object_features.shape[0])))
+            return [f"c{k}" for k in range(object_features.shape[0])], None
+
+        def decode_captions(self, ids):
+            return [str(r) for r in ids.tolist()]
+
+        def save(self, path):
+            open(path, "wb").close()
+            self.calls.append(("save", os.path.basename(path)))
+
+    def split(n_img, n_cap, seed):
+        r = np.random.default_rng(seed)
+        return {"features": r.random((n_img, 3, 8), dtype=np.float32),
+                "positions": r.random((n_img, 3, 5), dtype=np.float32),
+                "captions": r.integers(1, 9, (n_cap, 6)).astype(np.int32),
+                "image_idxs": r.integers(0, n_img, n_cap).astype(np.int32)}
+
+    m = Rec()
+    logs = []
+    hist = train(m, split(5, 23, 0), split(4, 9, 1), num_epoch=2, batch_size=4, output_path=str(tmp_path),
+                 eval_every=2, sample_every=5, log=logs.append, device="cpu", feature_dtype=torch.float32)
+    steps = [c for c in m.calls if c[0] == "step"]
+    assert len(steps) == 2 * 6 and steps[5] == ("step", 3)     # 23 captions / 4 -> 6 batches, last partial
+    # epoch 1: eval at steps 2,4,6 (2 losses each), a sample at step 5, then 3 zipped eval batches
+    e1 = m.calls[:m.calls.index(("save", "model_1.pt")) + 1]
+    assert sum(c[0] == "loss" for c in e1) == 3 * 2 + 3 * 2
+    assert ("gen", 1) in e1 and sum(c[0] == "gen" for c in e1) == 1 + 3
+    assert ("save", "model_2.pt") in m.calls and os.path.exists(tmp_path / "model" / "model_2.pt")
+    with open(tmp_path / "valid" / "valid.candidate.captions.pkl", "rb") as fh:
+        caps = pickle.load(fh)  # written by this test's own run
+    assert len(caps) == 4 and all(c.startswith("c") for c in caps if c)
+    assert len(hist) == 2 and hist[0]["loss"]["valid"] > 0
