@@ -772,11 +772,26 @@ struct capgen_engine {
       }
     }
   }
+  // FFN bias gradients (column sums of the ReLU'-masked hidden gradient) queued like the weight
+  // gradients: off the critical stream instead of as atomics in the dX GEMM's epilogue
+  // (CAPGEN_COLSUM_SIDE=0 restores the epilogue form)
+  struct ColJob {
+    const void* X;
+    int M, N;
+    float* db;
+  };
+  std::vector<ColJob> col_pending;
+  bool colsum_side = [] {
+    const char* e = std::getenv("CAPGEN_COLSUM_SIDE");
+    return !(e && e[0] == '0');
+  }();
   // es2 waits for everything issued on s so far, then runs the queued weight-gradient GEMMs
   void flush(hipStream_t s) {
     fork(s);
     dw_launch(dw_pending.data(), dw_pending.size(), es2);
     dw_pending.clear();
+    for (const ColJob& j : col_pending) column_sum(j.X, j.M, j.N, j.N, 1.f, nullptr, j.db, act, es2, NSTRIPE, n_small);
+    col_pending.clear();
   }
 
   // lb = the block's LayerNorm backward (dy = grad wrt block output, d_res -> r_out, d_a -> gA);
@@ -786,7 +801,9 @@ struct capgen_engine {
     layernorm_bwd(lb, act, s);
     void* gA = lb.d_a;
     dw_side(gA, d, H, f, W2, f, M, d, f, nullptr, s);
-    linear_dx(gA, d, W2, f, gH, f, M, d, f, 0, H, nullptr, s, GS(b1));  // x relu'(H); db1 = colsum
+    const bool side = colsum_side && es2 != s;
+    linear_dx(gA, d, W2, f, gH, f, M, d, f, 0, H, nullptr, s, side ? nullptr : GS(b1));  // x relu'(H)
+    if (side) col_pending.push_back(ColJob{gH, M, f, GS(b1)});                           // db1 = colsum
     dw_side(gH, f, X, d, W1, d, M, f, d, nullptr, s);
     linear_dx(gH, f, W1, d, lb.d_res, d, M, f, d, 1, nullptr, nullptr, s);
   }
@@ -1030,6 +1047,7 @@ struct capgen_engine {
     // last two buckets (feature/position embedding, encoder LN / biases) run on the bucket
     // stream behind ONE event (each event record costs the critical stream ~5 us)
     const hipStream_t tail = bstep ? ec : s;
+    if (!bstep) join(s);  // queued bias column sums (es2) precede the fold below
     if (bstep) dep(s, ec, ev_b1);
     if (bstep && L.has_img) dep(es2, ec, ev_b2);
     stripe_reduce(GS(L.enc_lng), NSTRIPE, n_small, L.dec_lng - L.enc_lng, G(L.enc_lng), 0, tail);

@@ -614,8 +614,8 @@ def test_train_loop_end_to_end_on_device(tmp_path):
     from capgen.train import train
 
     cfg = preset("C1").replace(dropout=0.1)
-    w2i = {f"w{i}": i for i in range(cfg.num_vocab)}
-    w2i.update({"<NULL>": 0, "<START>": 1, "<END>": 2})
+    w2i = {"<NULL>": 0, "<START>": 1, "<END>": 2}
+    w2i.update({f"w{i}": i for i in range(3, cfg.num_vocab)})
 
     def split(n_img, n_cap, seed):
         f, p, c = synthetic_batch(n_img, 8, cfg.encode_dim_features, cfg.encode_dim_positions, 10,
