@@ -27,7 +27,8 @@ inline void require(bool ok, const std::string& what) {
 
 // Diagnostic only (CAPGEN_SKIP bitmask, never set in production): skip a kernel class to
 // measure its marginal cost on the step's critical path.  1 LN fwd, 2 attention fwd, 4 LN bwd,
-// 8 attention bwd, 16 GEMM f32-out (weight gradients + classifier), 32 Adam, 64 bf16 GEMMs.
+// 8 attention bwd, 16 GEMM f32-out (weight gradients + classifier), 32 Adam, 64 bf16 GEMMs,
+// 128 LayerNorm-backward gamma/beta/bias sums.
 int skip_mask();
 
 // ---- scalar conversions -------------------------------------------------------------

@@ -206,8 +206,10 @@ static void ln_bwd_dispatch(const LnBwd& a, hipStream_t s) {
     default: throw Error("layernorm: width must be 64 * {1,2,4,8,16}");
   }
 }
-void layernorm_bwd(const LnBwd& a, DType t, hipStream_t s) {
-  if (a.M <= 0 || (skip_mask() & 4)) return;
+void layernorm_bwd(const LnBwd& a_in, DType t, hipStream_t s) {
+  if (a_in.M <= 0 || (skip_mask() & 4)) return;
+  LnBwd a = a_in;
+  if (skip_mask() & 128) a.dgamma = a.dbeta = a.dbias = nullptr;  // diagnostic: no parameter-gradient sums
   if (t == DType::F32) ln_bwd_dispatch<float>(a, s);
   else ln_bwd_dispatch<bf16>(a, s);
   CAPGEN_HIP(hipGetLastError());
