@@ -832,6 +832,11 @@ struct capgen_engine {
   // every producer of the bucket's gradients (consecutive buckets after one flush)
   // from_s: every producer of the bucket's gradients ran on s (no flush, ec waits for s)
   bool bstep = false;
+  // transformer blocks per gradient bucket (one flush = one event record on the critical stream)
+  int bucket_blocks = [] {
+    const char* e = std::getenv("CAPGEN_BUCKET_BLOCKS");
+    return e ? std::max(1, std::atoi(e)) : 1;
+  }();
   void bucket(int64_t off, int64_t n, hipStream_t s, bool sync = true, bool from_s = false) {
     if (sync && !from_s) flush(s);
     if (!bstep) return;
@@ -995,7 +1000,8 @@ struct capgen_engine {
       attention_bwd(g, A.Ps, gb.gATT1, gb.gQKV, at(gb.gQKV, dd), at(gb.gQKV, 2 * dd), act, s);
       dw_side(gb.gQKV, 3 * dd, a.D[l], dd, w.Wqkv, dd, Md, 3 * dd, dd, nullptr, s);
       linear_dx(gb.gQKV, 3 * dd, w.Wqkv, dd, gR, dd, Md, 3 * dd, dd, 1, nullptr, nullptr, s);
-      bucket(w.Wqkv, dec_end(l) - w.Wqkv, s);
+      if (l % bucket_blocks == 0)  // blocks l .. l + bucket_blocks - 1 (contiguous in the arena)
+        bucket(w.Wqkv, dec_end(std::min(l + bucket_blocks - 1, L.Ld - 1)) - w.Wqkv, s);
       std::swap(gO, gR);  // gO = grad wrt D_l
     }
     // cross K/V of all decoder blocks -> encoder output (the encoder chain starts here; the
@@ -1030,7 +1036,7 @@ struct capgen_engine {
     for (int l = L.Le - 1; l >= 0; --l) {
       const auto& w = L.enc[l];
       enc_layer_bwd(w, a.enc[l], a.genc[l], a.X[l], B, N, cfg.encode_mask ? a.valid : nullptr, l, on, gO, gR, s);
-      bucket(w.Wqkv, enc_end(l) - w.Wqkv, s);
+      if (l % bucket_blocks == 0) bucket(w.Wqkv, enc_end(std::min(l + bucket_blocks - 1, L.Le - 1)) - w.Wqkv, s);
     }
     // the tail of the step's dependency chain: the encoder-embedding LayerNorm backward and
     // weight gradient, then its Adam, which the next forward's first GEMM needs -- on the
