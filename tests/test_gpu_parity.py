@@ -239,9 +239,9 @@ def test_grouped_weight_gradients_match_single_launches_bf16(monkeypatch):
         e.forward(f, p, c)
         e.backward()
     ga, gb = a.grads_state_dict(), b.grads_state_dict()
-    for n in ga:
-        x, y = ga[n].double(), gb[n].double()
-        assert ((x - y).norm() / (x.norm() + 1e-12)).item() < 1e-4, n
+    rel = {n: ((ga[n].double() - gb[n].double()).norm() / (ga[n].double().norm() + 1e-12)).item() for n in ga}
+    bad = {n: r for n, r in rel.items() if r >= 1e-4}
+    assert not bad, (len(bad), len(rel), sorted(bad.items(), key=lambda kv: -kv[1])[:8])
 
 
 @pytest.mark.parametrize("graph", [False, True])
