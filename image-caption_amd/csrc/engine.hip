@@ -118,6 +118,8 @@ struct GenWS {
   int64_t *seq, *seq2;   // beam [R][Tw]
   float *bprob, *bprob2;
   int32_t *bsrc, *btok;
+  int64_t* out_ids;  // staged outputs of a graph-replayed decode: ids [R][maxlen + 1]
+  float* out_attn;   // greedy attention_list [maxlen - 1][R][N]
 };
 
 __global__ void init_gen_ids_kernel(int64_t* out, int rows, int width, int32_t* ids, int tcap) {
@@ -545,6 +547,72 @@ struct capgen_engine {
       (void)hipGraphExecDestroy(fexec);
       fexec = nullptr;
     }
+    drop_gen_graph();
+  }
+  void drop_gen_graph() {
+    for (auto& e : gen_graphs) (void)hipGraphExecDestroy(e.second);
+    gen_graphs.clear();
+    gen_seen.clear();
+  }
+
+  // Decoding as one replayed hipGraph: the first call with a given
+  // (kind, inputs, shape) runs eagerly (autotunes the GEMMs, sizes the workspaces), the second
+  // captures the whole encode + T-1 decode steps on the engine stream, later ones replay it.
+  // Outputs are staged in the workspace (g.out_*) and copied to the caller's buffers after
+  // the launch, so a new output tensor per call does not defeat the replay.
+  struct GenKey {
+    int kind;  // 0 greedy, 1 greedy + attention, 2 beam
+    const void *f, *p;
+    int ft, B, N, k;
+    bool operator==(const GenKey& o) const {
+      return kind == o.kind && f == o.f && p == o.p && ft == o.ft && B == o.B && N == o.N && k == o.k;
+    }
+  };
+  // off by default: measured slower than eager issue on MI355X / ROCm 7 (C4 B=256: beam 5
+  // 22.6 vs 21.9 ms, greedy 12.4 vs 11.6 ms, tools/bench_generate.py); CAPGEN_GEN_GRAPH=1 enables
+  bool gen_graph_on = [] {
+    const char* e = std::getenv("CAPGEN_GEN_GRAPH");
+    return e && e[0] == '1';
+  }();
+  static constexpr size_t kGenGraphs = 8;  // cached decode graphs (oldest evicted)
+  std::vector<std::pair<GenKey, hipGraphExec_t>> gen_graphs;
+  std::vector<GenKey> gen_seen;  // keys run eagerly once (next call captures)
+  template <class F>
+  void gen_run(const GenKey& k, F&& body, hipStream_t s) {
+    if (!gen_graph_on) return body();
+    for (auto& e : gen_graphs)
+      if (e.first == k) {
+        CAPGEN_HIP(hipGraphLaunch(e.second, s));
+        return;
+      }
+    if (std::find(gen_seen.begin(), gen_seen.end(), k) == gen_seen.end()) {  // first sighting: eager
+      body();
+      gen_seen.push_back(k);
+      if (gen_seen.size() > kGenGraphs) gen_seen.erase(gen_seen.begin());
+      return;
+    }
+    const GenWS saved = g;  // beam's host-side ping-pong swaps are replayed from this state
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    CAPGEN_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    try {
+      body();
+    } catch (...) {
+      (void)hipStreamEndCapture(s, &graph);
+      if (graph) (void)hipGraphDestroy(graph);
+      g = saved;
+      throw;
+    }
+    CAPGEN_HIP(hipStreamEndCapture(s, &graph));
+    g = saved;
+    CAPGEN_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    CAPGEN_HIP(hipGraphDestroy(graph));
+    if (gen_graphs.size() >= kGenGraphs) {
+      (void)hipGraphExecDestroy(gen_graphs.front().second);
+      gen_graphs.erase(gen_graphs.begin());
+    }
+    gen_graphs.emplace_back(k, exec);
+    CAPGEN_HIP(hipGraphLaunch(exec, s));
   }
 
   // ------------------------------------------------------------------------------------
@@ -1288,6 +1356,8 @@ struct capgen_engine {
     p.take(g.bprob2, R);
     p.take(g.bsrc, R);
     p.take(g.btok, R);
+    p.take(g.out_ids, (size_t)R * (Tc + 1));
+    p.take(g.out_attn, (size_t)(Tc - 1) * R * N);
   }
   void ensure_gen(int R, int N) {
     if (gws && R <= g.R && N <= g.N) return;
@@ -1296,6 +1366,7 @@ struct capgen_engine {
       CAPGEN_HIP(hipStreamSynchronize(es));
       CAPGEN_HIP(hipFree(gws));
       gws = nullptr;
+      drop_gen_graph();
     }
     Planner p;
     plan_gen(p, nR, nN);
@@ -1371,6 +1442,18 @@ struct capgen_engine {
   void greedy(const void* feats, DType ft, const float* pos, int B, int N, int64_t* ids_out, float* attn_out,
               hipStream_t s) {
     require(N >= 1 && N <= 64, "greedy: N must be in [1, 64]");
+    require(B >= 1, "greedy: need B >= 1");
+    ensure_acts(B, N, 2);
+    ensure_gen(B, N);
+    const GenKey key{attn_out ? 1 : 0, feats, pos, (int)ft, B, N, 0};
+    gen_run(key, [&] { greedy_body(feats, ft, pos, B, N, g.out_ids, attn_out ? g.out_attn : nullptr, s); }, s);
+    CAPGEN_HIP(hipMemcpyAsync(ids_out, g.out_ids, sizeof(int64_t) * B * (L.maxlen + 1), hipMemcpyDeviceToDevice, s));
+    if (attn_out)
+      CAPGEN_HIP(hipMemcpyAsync(attn_out, g.out_attn, sizeof(float) * (L.maxlen - 1) * B * N, hipMemcpyDeviceToDevice,
+                                s));
+  }
+  void greedy_body(const void* feats, DType ft, const float* pos, int B, int N, int64_t* ids_out, float* attn_out,
+                   hipStream_t s) {
     encode_only(feats, ft, pos, B, N, s);
     ensure_gen(B, N);
     const int Tc = L.maxlen, W = L.maxlen + 1;
@@ -1386,6 +1469,14 @@ struct capgen_engine {
   void beam(const void* feats, DType ft, const float* pos, int B, int N, int k, int64_t* ids_out, hipStream_t s) {
     require(k >= 1 && k <= 16, "beam_search: beam_size must be in [1, 16]");
     require(k <= L.V, "beam_search: beam_size must be <= num_vocab");
+    require(B >= 1 && N >= 1 && N <= 64, "beam_search: need B >= 1 and N in [1, 64]");
+    ensure_acts(B, N, 2);
+    ensure_gen(k * B, N);
+    const GenKey key{2, feats, pos, (int)ft, B, N, k};
+    gen_run(key, [&] { beam_body(feats, ft, pos, B, N, k, g.out_ids, s); }, s);
+    CAPGEN_HIP(hipMemcpyAsync(ids_out, g.out_ids, sizeof(int64_t) * B * L.maxlen, hipMemcpyDeviceToDevice, s));
+  }
+  void beam_body(const void* feats, DType ft, const float* pos, int B, int N, int k, int64_t* ids_out, hipStream_t s) {
     const int R = k * B, Tc = L.maxlen, Tw = L.maxlen, dd = L.dd;
     encode_only(feats, ft, pos, B, N, s);
     ensure_gen(R, N);

@@ -638,3 +638,37 @@ def test_train_loop_end_to_end_on_device(tmp_path):
         [n for n, _ in reference_param_specs(m.config)]
     with open(tmp_path / "valid" / "valid.candidate.captions.pkl", "rb") as fh:
         assert len(pickle.load(fh)) == 6  # written by this test's own run
+
+
+@pytest.mark.parametrize("tag", ["c1", "c2s", "c1_imgobj", "c1_movefirst"])
+def test_decode_graph_replay_matches_eager(tag, monkeypatch):
+    """Greedy and beam decoding replayed as captured hipGraphs (1st call eager, 2nd captures,
+    later ones replay) equal the eager engine bit for bit, match the reference fixtures, and
+    read the CURRENT weights after an Adam step in between."""
+    cfg, seed, z = load_fixture(tag)
+    f, p, c = _inputs(z)
+    monkeypatch.setenv("CAPGEN_GEN_GRAPH", "1")
+    a = _engine(cfg, seed)
+    monkeypatch.setenv("CAPGEN_GEN_GRAPH", "0")
+    b = _engine(cfg, seed)
+    monkeypatch.delenv("CAPGEN_GEN_GRAPH")
+    for e in (a, b):
+        e.set_training(False)
+        e.forward(f, p, c)  # size the training workspace first: no reallocation inside the loop
+        e.backward()
+    k = int(z["beam_k"]) or 3
+    for it in range(4):
+        ia, aa = a.greedy(f, p)
+        ib, ab = b.greedy(f, p)
+        ba, bb = a.beam(f, p, k), b.beam(f, p, k)
+        torch.cuda.synchronize()
+        assert torch.equal(ia, ib) and torch.equal(aa, ab) and torch.equal(ba, bb), it
+        if it == 0:
+            np.testing.assert_array_equal(ia.cpu().numpy(), z["greedy_ids"])
+            if int(z["beam_k"]):
+                np.testing.assert_array_equal(ba.cpu().numpy(), z["beam_ids"])
+        if it == 1:  # weights move: the graphs captured in this iteration must read the new ones
+            for e in (a, b):
+                e.forward(f, p, c)
+                e.backward()
+                e.adam_step()
