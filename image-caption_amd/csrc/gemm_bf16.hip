@@ -547,8 +547,17 @@ static Choice tune(const GemmArgs& g, hipStream_t s) {
   Choice best{heuristic_variant(g), 1};
   float best_ms = 1e30f;
   const int nk = (g.K + BK - 1) / BK;
+  // split-K factor cap (CAPGEN_MAX_SPLITK, default 2).  With factors up to 8 the c2s train step
+  // was not reproducible run to run (tools/step_det_probe.py: encoder gradients of two identical
+  // engines differed by ~3e-3 relative in ~1 of 5 runs; 1 of 16 at cap 4, 0 of 48 at cap 2,
+  // 0 of 16 without split-K); the combine sums slices in a fixed order, the root cause is open
+  // (DESIGN.md section 6).  Cap 2 costs ~0.05 ms of the 3.4 ms C2 step vs cap 8.
+  static const int max_sk = [] {
+    const char* e = std::getenv("CAPGEN_MAX_SPLITK");
+    return e ? std::max(1, std::atoi(e)) : 2;
+  }();
   for (int sk : {1, 2, 3, 4, 6, 8}) {
-    if (sk > 1 && nk < 4 * sk) break;
+    if (sk > max_sk || (sk > 1 && nk < 4 * sk)) break;
     if (sk > 1) ensure_ws(s, splitk_bytes(g, sk));
     for (int v = 1; v <= NVARIANTS; ++v) {
       launch_variant<TO, TA, TB>(v, t, s, sk);  // warm-up
