@@ -442,6 +442,15 @@ static void launch_cfg(const GemmArgs& g, hipStream_t s, int splitk) {
     require(w.bytes >= bytes && w.cnt, "gemm: split-K workspace too small (tune outside capture)");
     require(tn * tm <= kMaxTiles, "gemm: too many tiles for split-K");
     ws = w.p, cnt = w.cnt;
+    // CAPGEN_SPLITK_MEMSET=1: zero the tickets on the launching stream before every split-K
+    // launch (the guide's recipe) instead of relying on the last arriver's reset alone.  Probe:
+    // 0 of 20 vs 4 of 20 non-reproducible c2s steps at split-K 8, but a test still diverged once
+    // with it and it costs ~0.07 ms per step, so it stays off pending the root cause
+    static const bool zero_each = [] {
+      const char* e = std::getenv("CAPGEN_SPLITK_MEMSET");
+      return e && e[0] == '1';
+    }();
+    if (zero_each) CAPGEN_HIP(hipMemsetAsync(cnt, 0, (size_t)tn * tm * sizeof(int), s));
   }
   // group_m ~ sqrt(tiles per XCD), so each XCD's tile block is about square
   static const bool grouping = [] {
