@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcapgen.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 F32, BF16 = 0, 1
 
@@ -69,6 +69,9 @@ _SIGS = {
     "capgen_debug_gemm": (C.c_int, [C.c_int, C.c_int, C.c_int, _P, C.c_int64, C.c_int, _P, C.c_int64, C.c_int,
                                     _P, C.c_int64, C.c_int, C.c_int, _P, C.c_float, C.c_int, C.c_int, _P]),
     "capgen_debug_gemm_variant": (C.c_int, [C.c_int]),
+    "capgen_debug_splitk_protocol": (C.c_int, [C.c_int]),
+    "capgen_debug_splitk_diag": (C.c_int, [_P, C.c_int]),
+    "capgen_debug_copy_buffer": (C.c_int, [_P, C.c_int, _P, C.c_int64]),
     "capgen_train_step_indexed": (C.c_int, [_P, _P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int, _P,
                                             _P]),
     "capgen_rl_sample": (C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P]),

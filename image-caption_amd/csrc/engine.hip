@@ -878,7 +878,15 @@ struct capgen_engine {
   // MHA output projection + LayerNorm backward: lb as above (d_res = grad wrt the residual /
   // query input); writes grad wrt the attention output into gATT.
   void mha_out_bwd(int M, int d, const LnBwd& lb, const void* att, int64_t Wo, void* gATT, hipStream_t s) {
+    const bool snap = dbg_stop == 4 && dbg_snap_on;  // diagnostic snapshots (tools/bwd_bisect.py)
+    if (snap) {
+      CAPGEN_HIP(hipMemcpyAsync(dbg_snap[0], lb.dy, (size_t)M * d * es_(), hipMemcpyDeviceToDevice, s));
+      CAPGEN_HIP(hipMemcpyAsync(dbg_snap[2], lb.v, (size_t)M * d * es_(), hipMemcpyDeviceToDevice, s));
+      CAPGEN_HIP(hipMemcpyAsync(dbg_snap[3], lb.mean, (size_t)M * 4, hipMemcpyDeviceToDevice, s));
+      CAPGEN_HIP(hipMemcpyAsync(dbg_snap[4], lb.rstd, (size_t)M * 4, hipMemcpyDeviceToDevice, s));
+    }
     layernorm_bwd(lb, act, s);
+    if (snap) CAPGEN_HIP(hipMemcpyAsync(dbg_snap[1], lb.d_a, (size_t)M * d * es_(), hipMemcpyDeviceToDevice, s));
     dw_side(lb.d_a, d, att, d, Wo, d, M, d, d, nullptr, s);
     linear_dx(lb.d_a, d, Wo, d, gATT, d, M, d, d, 0, nullptr, nullptr, s);
   }
@@ -900,6 +908,15 @@ struct capgen_engine {
   // every producer of the bucket's gradients (consecutive buckets after one flush)
   // from_s: every producer of the bucket's gradients ran on s (no flush, ec waits for s)
   bool bstep = false;
+  // diagnostic: backward stops early (1: after the encoder-output gradient GEMM, 2: after the last
+  // encoder block's FFN backward, 3: after that whole block) so capgen_debug_copy_buffer can
+  // compare intermediate gradients run to run (tools/bwd_bisect.py)
+  void* dbg_snap[5] = {};  // stop 4: dy / d_a / v / mean / rstd of the last encoder block's MHA LayerNorm
+  bool dbg_snap_on = false;
+  int dbg_stop = [] {
+    const char* e = std::getenv("CAPGEN_DEBUG_BWD_STOP");
+    return e ? std::atoi(e) : 0;
+  }();
   // transformer blocks per gradient bucket (one flush = one event record on the critical stream)
   int bucket_blocks = [] {
     const char* e = std::getenv("CAPGEN_BUCKET_BLOCKS");
@@ -932,7 +949,12 @@ struct capgen_engine {
     const LnBwd lmha = lnb_desc(Me, d, gR, A.v1, A.m1, A.r1, w.ln1g, w.ln1b, -1, RowMask{},
                                 mk_drop(p, site(0, layer, 1), on), gO, gb.gA1);
     ffn_bwd(Me, d, L.fe, lffn, A.Y, A.H, w.W1, w.b1, w.W2, gb.gH, s);  // gR = grad wrt Y
+    if (dbg_stop == 2 && layer == L.Le - 1) return;
+    dbg_snap_on = layer == L.Le - 1;
+    if (dbg_stop == 4 && dbg_snap_on && !dbg_snap[0])
+      for (void*& q : dbg_snap) CAPGEN_HIP(hipMalloc(&q, (size_t)Me * d * es_()));
     mha_out_bwd(Me, d, lmha, A.att, w.Wo, gb.gATT1, s);
+    dbg_snap_on = false;
     AttnGeom g;
     g.B = B, g.H = He, g.Lq = N, g.Lk = N, g.dk = dke;
     g.q = A.qkv, g.q_ld = 3 * d, g.q_bs = (int64_t)N * 3 * d;
@@ -1092,6 +1114,7 @@ struct capgen_engine {
     gO = eO;
     gR = a.tmp;
     linear_dx(a.gKV, kvld, L.Wkv_all, d, gO, d, Me, L.Ld * 2 * dd, d, 0, nullptr, nullptr, s);
+    if (dbg_stop == 1) return join(s);  // diagnostic (CAPGEN_DEBUG_BWD_STOP): capgen_debug_copy_buffer
     if (L.has_mf) first_region_grad(a.mfGU, B, Lq, N, d, gO, act, s);  // enc[:, 0] of U = D + enc[:, 0]
     dw_side(a.gKV, kvld, a.X[L.Le], d, L.Wkv_all, d, Me, L.Ld * 2 * dd, d, nullptr, s);
     // the decoder-embedding branch (es2) has been issued: every decoder-side gradient is final
@@ -1104,6 +1127,7 @@ struct capgen_engine {
     for (int l = L.Le - 1; l >= 0; --l) {
       const auto& w = L.enc[l];
       enc_layer_bwd(w, a.enc[l], a.genc[l], a.X[l], B, N, cfg.encode_mask ? a.valid : nullptr, l, on, gO, gR, s);
+      if (dbg_stop >= 2 && l == L.Le - 1) return join(s);  // 3, 4: after the whole block
       if (l % bucket_blocks == 0) bucket(w.Wqkv, enc_end(std::min(l + bucket_blocks - 1, L.Le - 1)) - w.Wqkv, s);
     }
     // the tail of the step's dependency chain: the encoder-embedding LayerNorm backward and
@@ -1915,6 +1939,32 @@ int capgen_debug_attention(int dtype, int B, int H, int Lq, int Lk, int dk, cons
 
 int capgen_debug_gemm_variant(int v) {
   return guarded([&] { gemm_set_variant(v); });
+}
+
+int capgen_debug_copy_buffer(capgen_t* h, int which, void* host_dst, int64_t bytes) {
+  return guarded([&] {
+    set_device(h);
+    require(h->ws != nullptr, "debug_copy_buffer: no workspace yet");
+    const int Le = h->L.Le;
+    void* src = which == 0 ? h->a.tmp : which == 1 ? h->a.gOut : which == 2 ? h->a.gRes : which == 3 ? h->a.gKV
+              : which == 4 ? h->a.genc[Le - 1].gH : which == 5 ? h->a.genc[Le - 1].gAf
+              : which == 6 ? h->a.genc[Le - 1].gA1 : which == 7 ? h->a.genc[Le - 1].gQKV
+              : which >= 8 && which < 13 ? h->dbg_snap[which - 8] : nullptr;
+    require(src != nullptr, "debug_copy_buffer: which in 0..12 (8-12 need CAPGEN_DEBUG_BWD_STOP=4)");
+    CAPGEN_HIP(hipDeviceSynchronize());
+    CAPGEN_HIP(hipMemcpy(host_dst, src, (size_t)bytes, hipMemcpyDeviceToHost));
+  });
+}
+
+int capgen_debug_splitk_diag(int* out4, int reset) {
+  return guarded([&] { gemm_splitk_diag(out4, reset != 0); });
+}
+
+int capgen_debug_splitk_protocol(int proto) {
+  return guarded([&] {
+    require(proto >= 0 && proto < 1024, "debug_splitk_protocol: bits 0..9 only");
+    gemm_set_splitk_protocol(proto);
+  });
 }
 
 int capgen_dp_unique_id(char out[128]) {

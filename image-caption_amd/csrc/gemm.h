@@ -44,6 +44,10 @@ void gemm(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t 
 void gemm_init();
 // experiment hook: force a bf16 GEMM tile/wave/stage variant (0 = heuristic)
 void gemm_set_variant(int v);
+// diagnostic: split-K hand-off protocol bits (0 = the full recipe; gemm_bf16.hip g_splitk_proto)
+void gemm_set_splitk_protocol(int p);
+// diagnostic: read (and optionally zero) the split-K hand-off counters (protocol bit 64)
+void gemm_splitk_diag(int* out4, bool reset);
 // n <= kMaxGroup independent bf16-operand GEMMs of one layout / output type in one launch
 // (tile variant autotuned per group signature); no beta/colsum/alpha_ptr-free restrictions
 void gemm_grouped(const GemmArgs* probs, int n, DType out, bool ta, bool tb, hipStream_t s);

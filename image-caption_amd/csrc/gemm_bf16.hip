@@ -169,11 +169,15 @@ template <typename TO, int FM, int FN, int TM, int TN>
 __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&acc)[FM][FN], int m0, int n0, int wm,
                                               int wn, int lane, float alpha);
 
+// diagnostic counters of the split-K hand-off (protocol bit 64): [0] tickets found >= splitk at
+// arrival (a ticket not re-armed before this launch), [1] tiles combined
+__device__ int g_sk_diag[4];
+
 // One BMxBN output tile (split-K slice `split` of `splitk`) of C = op(A).op(B): the LDS-DMA
 // ring, the MFMA main loop and the epilogue (in-launch split-K combine included).
 template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int STAGES>
 __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int mt, int nt, int tile, int split, int splitk,
-                                          const void* zero, float* ws, int* tile_cnt, char* smem) {
+                                          const void* zero, float* ws, int* tile_cnt, char* smem, int proto = 0) {
   typedef TileCfg<TA, TB, BM, BN, WM, WN, STAGES> Cfg;
   constexpr int NW = Cfg::NW;
   typedef typename Cfg::OA OA;
@@ -236,12 +240,21 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int mt, int nt, int
   // ---- epilogue: lane holds C[m = mb + (lane&15)][n = nb + 4*(lane>>4) + 0..3] ----
   const float alpha = g.alpha_ptr ? g.alpha * *g.alpha_ptr : g.alpha;
   if (splitk > 1) {
-    // Split-K combine inside the launch (the guide's counter hand-off, write-through form):
-    // every slice stores its raw partial tile to the f32 workspace with 16-B sc1 buffer stores
-    // (write-through: no L2 write-back fence), every wave drains them, one lane takes a ticket
-    // (agent atomic); the block that draws the last ticket reads the other slices with sc1
-    // loads, sums all slices in slice order (deterministic whichever block is last) and runs
-    // the normal epilogue.  Correct for any placement of a tile's slices over XCDs.
+    // Split-K combine inside the launch (the guide's counter hand-off, cdna_hip_programming.md
+    // §5 'Projection GEMM' item 2 / §6 Guideline 16): every slice stores its raw partial tile
+    // to the f32 workspace with 16-B write-through (sc1) buffer stores (no release fence
+    // needed), every wave drains them (vmcnt(0)), the workgroup barrier, then ONE lane takes a
+    // ticket (agent atomic).  The block that draws the last ticket re-arms the ticket with an
+    // atomic exchange (performed where the adds are: a plain or sc1 store of 0 mixed with the
+    // atomic adds made later launches miscount, tools/step_det_probe.py) and runs ONE
+    // agent-scope acquire (drops this CU's stale L1 lines: several workgroups share a CU here)
+    // before any wave reads the other slices; it sums all slices in slice order (deterministic
+    // whichever block is last) and runs the normal epilogue.  Correct for any placement of a
+    // tile's slices over CUs / XCDs.
+    // `proto` (diagnostic, capgen_debug_splitk_protocol): bit 0 adds a writer release, bit 1
+    // drops the reader acquire, bit 2 reads the slabs with sc1 loads, bit 4 re-arms the ticket
+    // with a relaxed atomic store (the round-1 form was bits 1|2|4); bit 3 is the launcher's
+    // per-launch ticket memset.
     constexpr int NT = 64 * NW, NF = FM * FN;
     const int tid = threadIdx.x;
     const int64_t tile_bytes = (int64_t)splitk * NF * NT * 16;
@@ -252,20 +265,44 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int mt, int nt, int
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rsrc,
-                                               ((split * NF + i * FN + j) * NT + tid) * 16, 0, 16 /* sc1 */);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (proto & 512)  // diagnostic: system-scope (sc0 sc1) slab stores
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rsrc,
+                                                 ((split * NF + i * FN + j) * NT + tid) * 16, 0, 17);
+        else
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rsrc,
+                                                 ((split * NF + i * FN + j) * NT + tid) * 16, 0, 16 /* sc1 */);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
     __syncthreads();
-    volatile int* flag = reinterpret_cast<volatile int*>(smem);  // staging LDS is free now
+    typedef __attribute__((address_space(3))) volatile int lds_int;
+    lds_int* flag = (lds_int*)smem;  // staging LDS is free now
     if (tid == 0) {
+      if (proto & 1) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the fence's own wait can be dropped (G16 pitfall 12)
+      }
       const int old = __hip_atomic_fetch_add(tile_cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = old == splitk - 1;
-      if (last) __hip_atomic_store(tile_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+      if (proto & 64) {
+        if (old < 0 || old >= splitk) atomicAdd(&g_sk_diag[0], 1);
+        if (last) atomicAdd(&g_sk_diag[1], 1);
+      }
+      if (last) {
+        if (proto & 16) __hip_atomic_store(tile_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else (void)__hip_atomic_exchange(tile_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (proto & 128) {  // diagnostic: system-scope acquire
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if (!(proto & 2)) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // holds the barrier below until the invalidate is done
+        }
+      }
       *flag = last;
     }
     __syncthreads();
     if (!*flag) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 loads below the ticket
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the ticket
+    const int lpol = (proto & 256) ? 17 : (proto & 4) ? 16 /* sc1 */ : 0;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -275,8 +312,10 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int mt, int nt, int
           if (sl == split) {
             sum += acc[i][j];
           } else {
-            const u32x4 o = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ((sl * NF + i * FN + j) * NT + tid) * 16, 0,
-                                                                  16 /* sc1 */);
+            const int off = ((sl * NF + i * FN + j) * NT + tid) * 16;
+            const u32x4 o = lpol == 17 ? __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 17)
+                            : lpol     ? __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 16)
+                                       : __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
             sum += __builtin_bit_cast(f32x4, o);
           }
         }
@@ -358,7 +397,7 @@ __device__ __forceinline__ int xcd_slot(int bid, int nblk) {
 template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int STAGES>
 __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmArgs g, int tiles_n, int nblk,
                                                                 const void* zero, int splitk, float* ws,
-                                                                int* tile_cnt, int group_m) {
+                                                                int* tile_cnt, int group_m, int proto) {
   __shared__ __attribute__((aligned(1024))) char smem[TileCfg<TA, TB, BM, BN, WM, WN, STAGES>::SMEM];
   const int slot = xcd_slot(blockIdx.x, nblk);
   const int tile = slot / splitk, split = slot % splitk;  // split-K slices of a tile are adjacent
@@ -370,7 +409,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmArgs g, int
     const int gsz = min(tiles_m - first, group_m), r = tile % per;
     mt = first + r % gsz, nt = r / gsz;
   }
-  gemm_tile<TO, TA, TB, BM, BN, WM, WN, STAGES>(g, mt, nt, tile, split, splitk, zero, ws, tile_cnt, smem);
+  gemm_tile<TO, TA, TB, BM, BN, WM, WN, STAGES>(g, mt, nt, tile, split, splitk, zero, ws, tile_cnt, smem, proto);
 }
 
 // Grouped launch: up to kMaxGroup independent GEMMs of one layout (e.g. every weight gradient
@@ -401,6 +440,13 @@ struct Workspace {
 };
 constexpr int kMaxTiles = 1 << 16;
 std::map<hipStream_t, Workspace> g_ws;
+// split-K hand-off protocol (diagnostic; 0 = production, see gemm_tile): bit 0 writer release,
+// bit 1 no reader acquire, bit 2 sc1 slab loads, bit 3 per-launch ticket memset, bit 4 ticket
+// re-armed by a relaxed atomic store (round 1: 2|4|16)
+int g_splitk_proto = [] {
+  const char* e = std::getenv("CAPGEN_SPLITK_PROTO");
+  return e ? std::atoi(e) : 0;
+}();
 std::mutex g_ws_mu;
 
 // make sure the stream's split-K workspace holds `bytes` (never called inside a capture)
@@ -442,15 +488,16 @@ static void launch_cfg(const GemmArgs& g, hipStream_t s, int splitk) {
     require(w.bytes >= bytes && w.cnt, "gemm: split-K workspace too small (tune outside capture)");
     require(tn * tm <= kMaxTiles, "gemm: too many tiles for split-K");
     ws = w.p, cnt = w.cnt;
-    // CAPGEN_SPLITK_MEMSET=1: zero the tickets on the launching stream before every split-K
-    // launch (the guide's recipe) instead of relying on the last arriver's reset alone.  Probe:
-    // 0 of 20 vs 4 of 20 non-reproducible c2s steps at split-K 8, but a test still diverged once
-    // with it and it costs ~0.07 ms per step, so it stays off pending the root cause
-    static const bool zero_each = [] {
-      const char* e = std::getenv("CAPGEN_SPLITK_MEMSET");
-      return e && e[0] == '1';
-    }();
-    if (zero_each) CAPGEN_HIP(hipMemsetAsync(cnt, 0, (size_t)tn * tm * sizeof(int), s));
+    if (g_splitk_proto & 32) {  // diagnostic: rotate over 4 ticket arrays (kMaxTiles / 4 each)
+      static std::map<hipStream_t, int> rot;
+      cnt += (rot[s]++ & 3) * (kMaxTiles / 4);
+      require(tn * tm <= kMaxTiles / 4, "gemm: too many tiles for ticket rotation");
+    }
+    // tickets: zeroed once at allocation and re-armed by each tile's last arriver (an atomic
+    // exchange, gemm_tile); a per-launch memset (the guide's 'Re-initialise every call') costs
+    // 6-40 us per launch as a separate node on ROCm 7 (tools/splitk_stress.py time) -- diagnostic
+    // bit 8 of capgen_debug_splitk_protocol restores it
+    if (g_splitk_proto & 8) CAPGEN_HIP(hipMemsetAsync(cnt, 0, (size_t)(tn * tm + 3) / 4 * 16, s));
   }
   // group_m ~ sqrt(tiles per XCD), so each XCD's tile block is about square
   static const bool grouping = [] {
@@ -463,7 +510,7 @@ static void launch_cfg(const GemmArgs& g, hipStream_t s, int splitk) {
     group_m = std::max(1, std::min(tm, (int)std::lround(std::sqrt(per_xcd))));
   }
   gemm_bf16_kernel<TO, TA, TB, BM, BN, WM, WN, ST>
-      <<<nblk, 64 * WM * WN, 0, s>>>(g, tn, nblk, g_zero_page[dev], splitk, ws, cnt, group_m);
+      <<<nblk, 64 * WM * WN, 0, s>>>(g, tn, nblk, g_zero_page[dev], splitk, ws, cnt, group_m, g_splitk_proto & ~8);
 }
 
 // split-K workspace bound for any variant (tiles up to 256x128)
@@ -483,6 +530,26 @@ const char* kVariantName[NVARIANTS + 1] = {"auto",        "128x128w4s3", "128x12
                                            "64x64w4s4",   "64x64w4s6",   "128x64w4s4",   "64x128w4s4",
                                            "128x128w4s4", "32x64w4s2",   "64x32w4s2",    "32x32w4s2",
                                            "64x64w8s2",   "32x64w4s3",   "64x32w4s3"};
+
+// output tile width (columns) of each variant
+constexpr int kVariantBN[NVARIANTS + 1] = {0,  128, 128, 128, 64, 128, 64, 64, 64, 128, 128, 64,
+                                           64, 64,  64,  128, 128, 64, 32, 32, 64, 64,  32};
+
+// A tile whose output row segment is narrower than a 128-B cache line shares lines of C with
+// its neighbour tile, which another workgroup -- possibly on another XCD -- writes in the same
+// launch.  With a read-modify-write epilogue (beta: C is read first) each XCD's L2 then holds
+// the whole line with the neighbour's half stale, and a later kernel on that XCD can read the
+// stale half (measured: ~1 in 5 bf16 c2s backward passes differed run to run in the encoder
+// gradients, tools/bwd_bisect.py).  Such variants are never chosen, so every line of C is
+// written by exactly one workgroup.  CAPGEN_ALLOW_PARTIAL_LINES=1 lifts the rule (diagnostic).
+template <typename TO>
+static bool whole_lines(int v) {
+  static const bool allow = [] {
+    const char* e = std::getenv("CAPGEN_ALLOW_PARTIAL_LINES");
+    return e && e[0] == '1';
+  }();
+  return allow || kVariantBN[v] * (int)sizeof(TO) >= 128;
+}
 
 template <typename TO, bool TA, bool TB>
 static void launch_variant(int v, const GemmArgs& g, hipStream_t s, int sk = 1) {
@@ -556,19 +623,31 @@ static Choice tune(const GemmArgs& g, hipStream_t s) {
   Choice best{heuristic_variant(g), 1};
   float best_ms = 1e30f;
   const int nk = (g.K + BK - 1) / BK;
-  // split-K factor cap (CAPGEN_MAX_SPLITK, default 2).  With factors up to 8 the c2s train step
-  // was not reproducible run to run (tools/step_det_probe.py: encoder gradients of two identical
-  // engines differed by ~3e-3 relative in ~1 of 5 runs; 1 of 16 at cap 4, 0 of 48 at cap 2,
-  // 0 of 16 without split-K); the combine sums slices in a fixed order, the root cause is open
-  // (DESIGN.md section 6).  Cap 2 costs ~0.05 ms of the 3.4 ms C2 step vs cap 8.
+  // split-K factor cap (CAPGEN_MAX_SPLITK, default 8).  Round 1 capped it at 2 because the bf16
+  // step was not reproducible run to run with higher factors; the causes were a sub-line output
+  // tile under a read-modify-write epilogue (whole_lines) and the combine's ticket re-arm /
+  // missing acquire (gemm_tile) -- tools/step_det_probe.py: 0 of 60 diverging runs at cap 8 now.
   static const int max_sk = [] {
     const char* e = std::getenv("CAPGEN_MAX_SPLITK");
-    return e ? std::max(1, std::atoi(e)) : 2;
+    return e ? std::max(1, std::atoi(e)) : 8;
   }();
+  // diagnostic: CAPGEN_SPLITK_K=k1,k2,... allows split-K only for those K (bisecting a step)
+  static const std::vector<int> sk_only = [] {
+    std::vector<int> v;
+    if (const char* e = std::getenv("CAPGEN_SPLITK_K"))
+      for (const char* p = e; *p;) {
+        v.push_back(std::atoi(p));
+        while (*p && *p != ',') ++p;
+        if (*p) ++p;
+      }
+    return v;
+  }();
+  const bool sk_ok = sk_only.empty() || std::find(sk_only.begin(), sk_only.end(), g.K) != sk_only.end();
   for (int sk : {1, 2, 3, 4, 6, 8}) {
-    if (sk > max_sk || (sk > 1 && nk < 4 * sk)) break;
+    if (sk > max_sk || (sk > 1 && (nk < 4 * sk || !sk_ok))) break;
     if (sk > 1) ensure_ws(s, splitk_bytes(g, sk));
     for (int v = 1; v <= NVARIANTS; ++v) {
+      if (!whole_lines<TO>(v)) continue;
       launch_variant<TO, TA, TB>(v, t, s, sk);  // warm-up
       CAPGEN_HIP(hipEventRecord(e0, s));
       for (int r = 0; r < 3; ++r) launch_variant<TO, TA, TB>(v, t, s, sk);
@@ -712,6 +791,7 @@ static void launch_group(const GemmArgs* ps, int n, hipStream_t s) {
         CAPGEN_HIP(hipEventCreate(&e1));
         float best = 1e30f;
         for (int cand : kGroupVariants) {
+          if (!whole_lines<TO>(cand)) continue;
           launch_group_variant<TO, TA, TB>(cand, t.data(), n, s);
           CAPGEN_HIP(hipEventRecord(e0, s));
           for (int r = 0; r < 3; ++r) launch_group_variant<TO, TA, TB>(cand, t.data(), n, s);
@@ -758,6 +838,15 @@ void gemm_grouped(const GemmArgs* ps, int n, DType out, bool ta, bool tb, hipStr
 }
 
 void gemm_set_variant(int v) { g_variant = v; }
+void gemm_set_splitk_protocol(int p) { g_splitk_proto = p; }
+void gemm_splitk_diag(int* out4, bool reset) {
+  CAPGEN_HIP(hipDeviceSynchronize());
+  CAPGEN_HIP(hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_sk_diag), 4 * sizeof(int)));
+  if (reset) {
+    const int z[4] = {0, 0, 0, 0};
+    CAPGEN_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_sk_diag), z, sizeof(z)));
+  }
+}
 
 void gemm_init() {
   int dev = 0;
@@ -776,6 +865,9 @@ void gemm_bf16(const GemmArgs& g, DType out, bool ta, bool tb, hipStream_t s) {
   require(g_zero_page[dev] != nullptr, "gemm: gemm_init() not called on this device");
   require(g.N % 4 == 0 && g.ldc % 4 == 0 && (g.aux == nullptr || g.ldaux % 4 == 0),
           "gemm(bf16): N/ldc must be multiples of 4");
+  // read-modify-write epilogue: every 128-B line of C must belong to one tile (whole_lines)
+  require(!g.beta || (((uintptr_t)g.C & 127) == 0 && (g.ldc * (int64_t)dsize(out)) % 128 == 0),
+          "gemm(bf16): beta=1 needs C rows 128-B aligned (one writer per cache line)");
   if (out == DType::F32) launch_bf16_layout<float>(g, ta, tb, s);
   else launch_bf16_layout<bf16>(g, ta, tb, s);
 }

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define CAPGEN_ABI_VERSION 3
+#define CAPGEN_ABI_VERSION 4
 
 typedef struct capgen_engine capgen_t;
 
@@ -137,6 +137,20 @@ int capgen_debug_gemm(int M, int N, int K, const void* A, int64_t lda, int ta, c
 
 /* Experiment hook: force a GEMM tile/wave/pipeline variant (0 = production heuristic). */
 int capgen_debug_gemm_variant(int variant);
+/* Diagnostic hook: the in-launch split-K combine's hand-off protocol (0 = the production form:
+ * sc1 slab stores, agent acquire + plain slab loads in the combining workgroup, tickets re-armed
+ * by the last arriver's atomic exchange).  Bits: 1 adds a writer release fence, 2 drops the
+ * reader acquire, 4 reads the slabs with sc1 loads, 8 zeroes the tickets with a memset before
+ * every launch, 16 re-arms tickets with a relaxed atomic store (round 1 = 2|4|16;
+ * tools/splitk_stress.py, tools/step_det_probe.py). */
+int capgen_debug_splitk_protocol(int proto);
+/* Diagnostic: split-K hand-off counters collected under protocol bit 64 (out4[0] = tickets found
+ * out of range at arrival, out4[1] = tiles combined); synchronises the device; reset != 0 zeroes. */
+int capgen_debug_splitk_diag(int* out4, int reset);
+/* Diagnostic: synchronous copy of an internal gradient buffer (0 tmp, 1 gOut, 2 gRes, 3 cross-K/V
+ * gradient, 4-7 the last encoder block's FFN-hidden / FFN-LN / MHA-LN / QKV gradients) to host;
+ * with CAPGEN_DEBUG_BWD_STOP the backward pass ends early (tools/bwd_bisect.py). */
+int capgen_debug_copy_buffer(capgen_t* h, int which, void* host_dst, int64_t bytes);
 
 /* Training step over an HBM-resident feature store (replaces TrainDataset.__getitem__ + the
  * DataLoader collate + `.to(DEVICE)`, dataset.py:12-18, main.py:37-43, models.py:120-122):

@@ -27,6 +27,10 @@ def diff(sa, sb):
             if sa[k].dim() == 2 and k != "decoder.word_embedding.weight" and not torch.equal(sa[k], sb[k])]
 
 
+if os.environ.get("PROBE_PROTO"):  # split-K hand-off protocol bits (capgen_debug_splitk_protocol)
+    from capgen import _lib
+    _lib.check(_lib.load().capgen_debug_splitk_protocol(int(os.environ["PROBE_PROTO"])))
+n_diff = 0
 for it in range(int(sys.argv[1]) if len(sys.argv) > 1 else 6):
     a, b, c2 = mk(), mk(), mk()
     a.train_step(f, p, c)          # bucketed step
@@ -50,4 +54,17 @@ for it in range(int(sys.argv[1]) if len(sys.argv) > 1 else 6):
                        if "coder." in k else k for k, _, _ in d})
     print(f"iter {it}: step-vs-unfused {len(dab)} {short(dab)} | unfused-vs-unfused {len(dbc)} {short(dbc)}",
           flush=True)
+    n_diff += bool(dab or dbc)
+    if os.environ.get("PROBE_PROTO"):
+        import ctypes as C
+        from capgen import _lib
+        d4 = (C.c_int * 4)()
+        _lib.check(_lib.load().capgen_debug_splitk_diag(d4, 1))
+        print(f"iter {it}: split-K diag: out-of-range tickets {d4[0]}, tiles combined {d4[1]}", flush=True)
+    if dbc and n_diff <= 3:  # which gradients of the two unfused engines differ, in arena order
+        for k in gb:
+            r = ((gb[k].double() - gc[k].double()).norm() / (gb[k].double().norm() + 1e-30)).item()
+            if r > 0:
+                print(f"    grad {k}: rel {r:.2e}", flush=True)
     del a, b, c2
+print(f"SUMMARY proto={os.environ.get('PROBE_PROTO', 'default')} diverging iterations {n_diff}/{it + 1}", flush=True)
