@@ -2,7 +2,7 @@
 Transformer path of shao-chi/Image-Caption).  Host code here; kernels in libcapgen.so."""
 from .config import CapgenConfig, preset  # noqa: F401
 
-__all__ = ["CapgenConfig", "preset", "Engine", "Transformer", "TRANSFORMER"]
+__all__ = ["CapgenConfig", "preset", "Engine", "Transformer", "PolicyNetwork", "TRANSFORMER", "SelfCriticNetwork"]
 
 
 def __getattr__(name):
@@ -13,7 +13,13 @@ def __getattr__(name):
     if name == "Transformer":
         from .model import Transformer
         return Transformer
+    if name == "PolicyNetwork":
+        from .model import PolicyNetwork
+        return PolicyNetwork
     if name == "TRANSFORMER":
         from .models import TRANSFORMER
         return TRANSFORMER
+    if name == "SelfCriticNetwork":
+        from .models import SelfCriticNetwork
+        return SelfCriticNetwork
     raise AttributeError(name)

@@ -52,11 +52,13 @@ _SIGS = {
     "capgen_get_params": (C.c_int, [_P, _P, C.c_int64]),
     "capgen_set_params": (C.c_int, [_P, _P, C.c_int64]),
     "capgen_get_grads": (C.c_int, [_P, _P, C.c_int64]),
+    "capgen_set_grads": (C.c_int, [_P, _P, C.c_int64]),
     "capgen_get_adam_state": (C.c_int, [_P, C.POINTER(C.c_int64), _P, _P, C.c_int64]),
     "capgen_set_adam_state": (C.c_int, [_P, C.c_int64, _P, _P, C.c_int64]),
     "capgen_arenas": (C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), C.POINTER(C.c_int64)]),
     "capgen_set_training": (C.c_int, [_P, C.c_int]),
     "capgen_set_graph": (C.c_int, [_P, C.c_int]),
+    "capgen_set_decode_log_softmax": (C.c_int, [_P, C.c_int]),
     "capgen_forward": (C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int, _P, _P]),
     "capgen_backward": (C.c_int, [_P, _P]),
     "capgen_adam_step": (C.c_int, [_P, _P]),

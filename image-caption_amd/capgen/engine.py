@@ -58,6 +58,11 @@ class Engine:
         self.training = bool(training)
         _lib.check(self.lib.capgen_set_training(self.h, int(self.training)))
 
+    def set_decode_log_softmax(self, enable: bool):
+        """PolicyNetwork decoding (model_RL.py:72,126,182): greedy / beam score with LogSoftmax and
+        beams accumulate log-probabilities; False (default) = Transformer (Softmax, probabilities)."""
+        _lib.check(self.lib.capgen_set_decode_log_softmax(self.h, int(enable)))
+
     def set_graph(self, enable: bool):
         _lib.check(self.lib.capgen_set_graph(self.h, int(enable)))
 
@@ -85,6 +90,18 @@ class Engine:
     def grads_state_dict(self):
         torch.cuda.current_stream(self.device).synchronize()
         return self._unpack(self._arena_to_host(self.lib.capgen_get_grads))
+
+    def set_grads_arena(self, arena: np.ndarray):
+        """Overwrite the whole f32 gradient arena (layout: capgen_param_table) from host memory."""
+        a = np.ascontiguousarray(arena, dtype=np.float32)
+        assert a.size == self.arena_elems
+        torch.cuda.current_stream(self.device).synchronize()
+        _lib.check(self.lib.capgen_set_grads(self.h, a.ctypes.data_as(C.c_void_p), self.arena_elems))
+
+    def grads_arena(self) -> np.ndarray:
+        """The whole f32 gradient arena as a host copy."""
+        torch.cuda.current_stream(self.device).synchronize()
+        return self._arena_to_host(self.lib.capgen_get_grads)
 
     def load_state_dict(self, sd, strict: bool = True):
         arena = np.zeros(self.arena_elems, dtype=np.float32)

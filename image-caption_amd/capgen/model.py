@@ -132,6 +132,50 @@ class Transformer:
         return self.engine.grads_state_dict()
 
 
+class PolicyNetwork(Transformer):
+    """Drop-in for core/TRANSFORMER/model_RL.py:10-208 (the SCST model): the same encoder /
+    decoder / classifer weights as Transformer, but `forward` returns the logits (model_RL.py:
+    75-90), `sample` is argmax of LogSoftmax (:93-97), and decoding scores with LogSoftmax --
+    greedy takes argmax of it and beam search accumulates LOG-probabilities (:72,126,157,182),
+    where Transformer.beam_search adds probabilities (model.py:183)."""
+
+    def __init__(self, num_vocab, max_length, encode_dim_positions, encode_dim_features, device, pad_idx=0,
+                 dropout=0.2, encode_mask=False, encode_input_size=512, encode_q_k_dim=512, encode_v_dim=512,
+                 encode_hidden_size=2048, encode_num_blocks=6, encode_num_heads=8, dim_word_embedding=512,
+                 decode_input_size=512, decode_q_k_dim=512, decode_v_dim=512, decode_hidden_size=2048,
+                 decode_num_blocks=6, decode_num_heads=8, move_first_image_feature=False, **kw):
+        super().__init__(num_vocab, max_length, encode_dim_positions, encode_dim_features, device,
+                         output_name="RL_Transformer", encode_mask=encode_mask, pad_idx=pad_idx, dropout=dropout,
+                         encode_input_size=encode_input_size, encode_q_k_dim=encode_q_k_dim,
+                         encode_v_dim=encode_v_dim, encode_hidden_size=encode_hidden_size,
+                         encode_num_blocks=encode_num_blocks, encode_num_heads=encode_num_heads,
+                         dim_word_embedding=dim_word_embedding, decode_input_size=decode_input_size,
+                         decode_q_k_dim=decode_q_k_dim, decode_v_dim=decode_v_dim,
+                         decode_hidden_size=decode_hidden_size, decode_num_blocks=decode_num_blocks,
+                         decode_num_heads=decode_num_heads, move_first_image_feature=move_first_image_feature, **kw)
+        self.engine.set_decode_log_softmax(True)
+
+    @classmethod
+    def from_config(cls, cfg: CapgenConfig, device, state_dict=None):
+        obj = super().from_config(cfg, device, state_dict=state_dict)
+        obj.engine.set_decode_log_softmax(True)
+        return obj
+
+    def forward(self, object_features, position_features, target_caption):
+        """model_RL.py:75-90: teacher-forced logits [B, T-1, V] (f32, device)."""
+        self.engine.forward(object_features, position_features, target_caption)
+        B, T = target_caption.shape
+        return self.engine.logits(B, T)
+
+    __call__ = forward
+
+    @staticmethod
+    def sample(output):
+        """model_RL.py:93-97: (argmax of log_softmax, log_softmax)."""
+        log_probs = torch.log_softmax(output, dim=2)
+        return torch.argmax(log_probs, dim=2), log_probs
+
+
 class CapgenAdam:
     """optimizer.zero_grad()/step() for a capgen Transformer (torch.optim.Adam semantics,
     lr/betas/eps from the config).  zero_grad is free: backward overwrites the arena."""

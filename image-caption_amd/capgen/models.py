@@ -12,7 +12,7 @@ import numpy as np
 import torch
 
 from .config import CapgenConfig
-from .model import Transformer
+from .model import PolicyNetwork, Transformer
 from .utils import decode_captions, load_word_to_idx
 
 
@@ -101,7 +101,12 @@ class SelfCriticNetwork(MODEL_init):
     (1 - w) * CE + w * structure loss with CIDEr-D + BLEU-4 + entropy rewards (loss.py:31-220).
 
     One step = capgen_rl_sample (GPU) -> host scoring of the greedy-from-logits samples
-    (capgen/scst.py, parity unpinned) -> capgen_rl_finish (GPU: loss, backward, Adam)."""
+    (capgen/scst.py, parity unpinned) -> capgen_rl_finish (GPU: loss, backward, Adam).
+
+    df: CIDEr-D document frequencies.  The reference scores with CiderD(df='coco-val')
+    (loss.py:112), a table computed from the COCO validation references that the reference does
+    not ship; the default 'corpus' computes them from the references being scored (coco-caption's
+    corpus mode) and warns.  Pass df=(document_frequency, ref_len) to use a precomputed table."""
 
     def __init__(self, config: CapgenConfig | None = None, word_to_idx=None, word_to_idx_path=None,
                  device="cuda:0", state_dict=None, structure_loss_weight=0.5, cider_reward_weight=1.0,
@@ -111,7 +116,14 @@ class SelfCriticNetwork(MODEL_init):
         cfg = (config or CapgenConfig()).replace(num_vocab=self.num_vocab)
         self.config = cfg
         self.device = torch.device(device)
-        self.model = Transformer.from_config(cfg, self.device, state_dict=state_dict)
+        # PolicyNetwork (model_RL.py): generate_caption then decodes with LogSoftmax scoring
+        self.model = PolicyNetwork.from_config(cfg, self.device, state_dict=state_dict)
+        if isinstance(df, str) and df == "corpus":
+            import warnings
+            warnings.warn("capgen SelfCriticNetwork: CIDEr-D document frequencies from the scored references "
+                          "(df='corpus'); the reference uses CiderD(df='coco-val') (loss.py:112), whose table is "
+                          "not shipped with it -- pass df=(document_frequency, ref_len) for that reward",
+                          stacklevel=2)
         self.structure_loss_weight = float(structure_loss_weight)  # core/config.py:81-85
         self.scorer = RewardScorer(self.idx_to_word, cider_reward_weight, bleu_reward_weight, entropy_reward_weight,
                                    self_cider_reward_weight, df=df)

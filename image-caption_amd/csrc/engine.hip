@@ -86,7 +86,7 @@ struct Acts {
   std::vector<DecAct> dec;
   float* logits;
   void* dlogits;
-  float *loss_row, *grad_scale, *loss;
+  float *loss_row, *grad_scale, *loss, *loss_ce;
   // SCST (rl.hip): per-row sample / lse / logp[sample] / entropy, per-image entropy, scalars
   int32_t* rl_sample;
   float *rl_lse, *rl_logp, *rl_ent, *rl_ent_img, *rl_score, *rl_scal;
@@ -298,6 +298,7 @@ struct capgen_engine {
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
   float* count_host = nullptr;  // pinned: global count override
+  hipEvent_t ev_count = nullptr;  // recorded after the copy of count_host (host writes wait for it)
   bool count_override = false;
 
   // ------------------------------------------------------------------------------------
@@ -437,6 +438,7 @@ struct capgen_engine {
     p.take(a.loss_row, Md);
     p.take(a.grad_scale, 4);
     p.take(a.loss, 4);
+    p.take(a.loss_ce, 4);
     p.take(a.rl_sample, Md);
     p.take(a.rl_lse, Md);
     p.take(a.rl_logp, Md);
@@ -560,8 +562,11 @@ struct capgen_engine {
   // captures the whole encode + T-1 decode steps on the engine stream, later ones replay it.
   // Outputs are staged in the workspace (g.out_*) and copied to the caller's buffers after
   // the launch, so a new output tensor per call does not defeat the replay.
+  // decode scoring: false = Softmax, probabilities accumulated over beams (Transformer,
+  // model.py:124-128,183); true = LogSoftmax, log-probabilities (PolicyNetwork, model_RL.py:72,182)
+  bool decode_logsm = false;
   struct GenKey {
-    int kind;  // 0 greedy, 1 greedy + attention, 2 beam
+    int kind;  // 0 greedy, 1 greedy + attention, 2 beam (+ 8: log-softmax scoring)
     const void *f, *p;
     int ft, B, N, k;
     bool operator==(const GenKey& o) const {
@@ -698,8 +703,10 @@ struct capgen_engine {
     pack_encoder_input(feats, ft, pos, Me, L.F, L.P, L.Kp, a.Aenc, act, a.valid, s, in_idx, N, in_n_img);
     prepare_captions(caps, B, T, cfg.pad_idx, a.ids, a.tgt, a.count, s);
     if (comm) {
-      if (count_override)
+      if (count_override) {
         CAPGEN_HIP(hipMemcpyAsync(a.count, count_host, sizeof(float), hipMemcpyHostToDevice, s));
+        CAPGEN_HIP(hipEventRecord(ev_count, s));  // capgen_dp_set_global_count waits for this copy
+      }
       else
         NCCL_CHECK(ncclAllReduce(a.count, a.count, 1, ncclFloat, ncclSum, comm, s));
     }
@@ -777,7 +784,17 @@ struct capgen_engine {
     // ---- classifier + CE (model.py:93-96) ----
     linear(dec_out(), dd, L.Wc, dd, a.logits, L.V, DType::F32, Md, L.V, dd, P(L.bc), 0, s);
     cross_entropy_rows(a.logits, a.tgt, Md, L.V, cfg.pad_idx, a.loss_row, a.dlogits, act, s);
-    loss_finalize(a.loss_row, Md, a.count, cfg.focal_loss, loss_out ? loss_out : a.loss, a.grad_scale, s);
+    float* lo = loss_out ? loss_out : a.loss;
+    if (comm) {
+      // data parallel: the mean CE over the GLOBAL batch (model.py:76) is the sum of the ranks'
+      // partial sums / global count -- one 4-byte all-reduce, then the (Focal) loss and the
+      // gradient scale from it on every rank (FocalLoss transforms the global mean, loss.py:20-28)
+      loss_finalize(a.loss_row, Md, a.count, 0, a.loss_ce, nullptr, s, nullptr, /*partial=*/1);
+      NCCL_CHECK(ncclAllReduce(a.loss_ce, a.loss_ce, 1, ncclFloat, ncclSum, comm, s));
+      loss_finalize(nullptr, 0, a.count, cfg.focal_loss, lo, a.grad_scale, s, a.loss_ce);
+    } else {
+      loss_finalize(a.loss_row, Md, a.count, cfg.focal_loss, lo, a.grad_scale, s);
+    }
   }
 
   // ------------------------------------------------------------------------------------
@@ -1469,7 +1486,7 @@ struct capgen_engine {
     require(B >= 1, "greedy: need B >= 1");
     ensure_acts(B, N, 2);
     ensure_gen(B, N);
-    const GenKey key{attn_out ? 1 : 0, feats, pos, (int)ft, B, N, 0};
+    const GenKey key{(attn_out ? 1 : 0) + (decode_logsm ? 8 : 0), feats, pos, (int)ft, B, N, 0};
     gen_run(key, [&] { greedy_body(feats, ft, pos, B, N, g.out_ids, attn_out ? g.out_attn : nullptr, s); }, s);
     CAPGEN_HIP(hipMemcpyAsync(ids_out, g.out_ids, sizeof(int64_t) * B * (L.maxlen + 1), hipMemcpyDeviceToDevice, s));
     if (attn_out)
@@ -1486,7 +1503,7 @@ struct capgen_engine {
     for (int t = 0; t < L.maxlen - 1; ++t) {
       dec_step(B, B, N, t, g.cache, g.ids, attn_out != nullptr, s);
       if (attn_out) attention_head_mean(g.Pc, B, L.Hd, 1, N, 0, attn_out + (int64_t)t * B * N, s);
-      argmax_softmax(g.logits, B, L.V, ids_out, W, t + 1, g.ids + t + 1, Tc, s);
+      argmax_softmax(g.logits, B, L.V, ids_out, W, t + 1, g.ids + t + 1, Tc, s, decode_logsm);
     }
   }
 
@@ -1496,7 +1513,7 @@ struct capgen_engine {
     require(B >= 1 && N >= 1 && N <= 64, "beam_search: need B >= 1 and N in [1, 64]");
     ensure_acts(B, N, 2);
     ensure_gen(k * B, N);
-    const GenKey key{2, feats, pos, (int)ft, B, N, k};
+    const GenKey key{2 + (decode_logsm ? 8 : 0), feats, pos, (int)ft, B, N, k};
     gen_run(key, [&] { beam_body(feats, ft, pos, B, N, k, g.out_ids, s); }, s);
     CAPGEN_HIP(hipMemcpyAsync(ids_out, g.out_ids, sizeof(int64_t) * B * L.maxlen, hipMemcpyDeviceToDevice, s));
   }
@@ -1508,7 +1525,7 @@ struct capgen_engine {
     CAPGEN_HIP(hipGetLastError());
     // position 0: every beam holds <START>; top-k of beam 0's distribution (model.py:148-166)
     dec_step(R, B, N, 0, g.cache, g.ids, false, s);
-    softmax_rows(g.logits, R, L.V, g.probs, s);
+    softmax_rows(g.logits, R, L.V, g.probs, s, decode_logsm);
     beam_topk(g.probs, nullptr, 1, B, L.V, k, g.bprob, g.bsrc, g.btok, s);
     CAPGEN_HIP(hipMemsetAsync(g.bsrc, 0, sizeof(int32_t) * R, s));  // all beams descend from beam 0 at t = 0
     auto reorder = [&](int t) {
@@ -1531,7 +1548,7 @@ struct capgen_engine {
     reorder(0);
     for (int t = 1; t < Tw - 1; ++t) {
       dec_step(R, B, N, t, g.cache, g.ids, false, s);
-      softmax_rows(g.logits, R, L.V, g.probs, s);
+      softmax_rows(g.logits, R, L.V, g.probs, s, decode_logsm);
       beam_topk(g.probs, g.bprob, k, B, L.V, k, g.bprob2, g.bsrc, g.btok, s);
       std::swap(g.bprob, g.bprob2);
       reorder(t);
@@ -1551,7 +1568,7 @@ struct capgen_engine {
     if (ev_out) (void)hipEventDestroy(ev_out);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
-    for (hipEvent_t e : {ev_b1, ev_b2, ev_cj})
+    for (hipEvent_t e : {ev_b1, ev_b2, ev_cj, ev_count})
       if (e) (void)hipEventDestroy(e);
     if (ec && ec != es && ec != es2) (void)hipStreamSynchronize(ec), (void)hipStreamDestroy(ec);
     if (es2 && es2 != es) (void)hipStreamSynchronize(es2), (void)hipStreamDestroy(es2);
@@ -1653,6 +1670,7 @@ int capgen_create(const capgen_config* cfg, int device, capgen_t** out) {
     for (hipEvent_t* e : {&h->ev_b1, &h->ev_b2, &h->ev_cj})
       CAPGEN_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
+    CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_count, hipEventDisableTiming));
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming));
     CAPGEN_HIP(hipMalloc(&h->params, n * 4));
     CAPGEN_HIP(hipMalloc(&h->grads, n * 4));
@@ -1723,6 +1741,15 @@ int capgen_get_grads(capgen_t* h, float* dst, int64_t n) {
   });
 }
 
+int capgen_set_grads(capgen_t* h, const float* src, int64_t n) {
+  return guarded([&] {
+    set_device(h);
+    require(n == h->L.total, "set_grads: size mismatch");
+    CAPGEN_HIP(hipStreamSynchronize(h->es));
+    CAPGEN_HIP(hipMemcpy(h->grads, src, n * 4, hipMemcpyHostToDevice));
+  });
+}
+
 int capgen_get_adam_state(capgen_t* h, int64_t* step, float* m, float* v, int64_t n) {
   return guarded([&] {
     set_device(h);
@@ -1761,6 +1788,13 @@ int capgen_set_training(capgen_t* h, int training) {
   return guarded([&] {
     require(h != nullptr, "null engine handle");
     h->training = training != 0;
+  });
+}
+
+int capgen_set_decode_log_softmax(capgen_t* h, int enable) {
+  return guarded([&] {
+    require(h != nullptr, "null engine handle");
+    h->decode_logsm = enable != 0;
   });
 }
 
@@ -1979,7 +2013,6 @@ int capgen_dp_init(capgen_t* h, const char id[128], int rank, int world) {
   return guarded([&] {
     set_device(h);
     require(world >= 1 && rank >= 0 && rank < world, "dp_init: bad rank/world");
-    require(!h->cfg.focal_loss || world == 1, "dp_init: FocalLoss needs the global mean CE; not supported with DP");
     ncclUniqueId uid;
     std::memcpy(uid.internal, id, 128);
     if (h->comm) ncclCommDestroy(h->comm);
@@ -1995,7 +2028,9 @@ int capgen_dp_init(capgen_t* h, const char id[128], int rank, int world) {
 
 int capgen_dp_set_global_count(capgen_t* h, float count) {
   return guarded([&] {
-    require(h != nullptr, "null engine handle");
+    set_device(h);
+    // the previous step's asynchronous copy may still be queued: it must read the old value
+    CAPGEN_HIP(hipEventSynchronize(h->ev_count));
     h->count_override = count > 0.f;
     *h->count_host = count;
   });

@@ -68,9 +68,10 @@ void stripe_reduce(const float* S, int stripes, int64_t stride, int64_t n, float
 // per-row cross entropy: loss_row[m] = lse - logit[tgt], dlogits = softmax - onehot (unscaled, 0 for pad)
 void cross_entropy_rows(const float* logits, const int32_t* tgt, int M, int V, int pad, float* loss_row,
                         void* dlogits, DType t, hipStream_t s);
-// loss = sum(loss_row)/count (or FocalLoss of it); grad_scale = dloss/d(logit sums)
+// loss = sum(loss_row)/count (or FocalLoss of it); grad_scale = dloss/d(logit sums).
+// ce_in: the mean CE is given (all-reduced partials); partial: write sum(loss_row)/count only.
 void loss_finalize(const float* loss_row, int M, const float* count, int focal, float* loss_out,
-                   float* grad_scale, hipStream_t s);
+                   float* grad_scale, hipStream_t s, const float* ce_in = nullptr, int partial = 0);
 // Adam (torch.optim.Adam semantics).  step_buf: int64 step counter (incremented here).
 void adam_prepare(int64_t* step, float lr, float b1, float b2, float* scal, hipStream_t s);
 void adam_update(float* p, const float* g, float* m, float* v, size_t n, float b1, float b2, float eps,
@@ -78,9 +79,9 @@ void adam_update(float* p, const float* g, float* m, float* v, size_t n, float b
 void to_bf16(const float* src, bf16* dst, size_t n, hipStream_t s);
 // greedy: out token = argmax(softmax(logits[b])) (first index on ties)   (model.py:126-128)
 void argmax_softmax(const float* logits, int B, int V, int64_t* ids_out, int64_t ids_ld, int col,
-                    int32_t* next_ids, int64_t next_ld, hipStream_t s);
+                    int32_t* next_ids, int64_t next_ld, hipStream_t s, int logsm = 0);
 // softmax probabilities [B][V] (for beam search)
-void softmax_rows(const float* logits, int B, int V, float* probs, hipStream_t s);
+void softmax_rows(const float* logits, int B, int V, float* probs, hipStream_t s, int logsm = 0);
 void bump_seed(uint64_t* seed, hipStream_t s);
 
 }  // namespace capgen

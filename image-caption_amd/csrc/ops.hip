@@ -524,16 +524,23 @@ void cross_entropy_rows(const float* logits, const int32_t* tgt, int M, int V, i
   CAPGEN_HIP(hipGetLastError());
 }
 
+// CE mean over the (global) non-pad count and the FocalLoss transform (model.py:73-76,
+// loss.py:20-28, gamma = 2, applied to the already-averaged CE).  ce_in != null: the mean CE is
+// given (the data-parallel path all-reduces the per-rank partial sums first); partial: only
+// the per-rank partial mean sum(rows) / count is written to loss_out.
 __global__ void loss_finalize_kernel(const float* __restrict__ loss_row, int M, const float* count, int focal,
-                                     float* loss_out, float* grad_scale) {
+                                     const float* ce_in, int partial, float* loss_out, float* grad_scale) {
   __shared__ float sh[4];
   float acc = 0.f;
-  for (int c = threadIdx.x; c < M; c += 256) acc += loss_row[c];
+  if (!ce_in)
+    for (int c = threadIdx.x; c < M; c += 256) acc += loss_row[c];
   acc = block_sum(acc, sh);
   if (threadIdx.x == 0) {
     const float n = *count;
-    const float ce = acc / n;
-    if (focal) {  // loss.py:20-28 with gamma = 2
+    const float ce = ce_in ? *ce_in : acc / n;
+    if (partial) {
+      *loss_out = ce;
+    } else if (focal) {
       const float pt = expf(-ce);
       const float om = 1.f - pt;
       *loss_out = om * om * ce;
@@ -545,8 +552,8 @@ __global__ void loss_finalize_kernel(const float* __restrict__ loss_row, int M, 
   }
 }
 void loss_finalize(const float* loss_row, int M, const float* count, int focal, float* loss_out, float* grad_scale,
-                   hipStream_t s) {
-  loss_finalize_kernel<<<1, 256, 0, s>>>(loss_row, M, count, focal, loss_out, grad_scale);
+                   hipStream_t s, const float* ce_in, int partial) {
+  loss_finalize_kernel<<<1, 256, 0, s>>>(loss_row, M, count, focal, ce_in, partial, loss_out, grad_scale);
   CAPGEN_HIP(hipGetLastError());
 }
 
@@ -609,9 +616,12 @@ void to_bf16(const float* src, bf16* dst, size_t n, hipStream_t s) {
 }
 
 // ---- greedy / beam helpers ---------------------------------------------------------
+// logsm = 0: argmax of Softmax (Transformer, model.py:124-128); 1: of LogSoftmax
+// (PolicyNetwork, model_RL.py:72,126-127) -- the same token except where the rounding of the
+// two scores makes different near-ties
 __global__ void __launch_bounds__(256) argmax_softmax_kernel(const float* __restrict__ logits, int V,
                                                              int64_t* ids_out, int64_t ids_ld, int col,
-                                                             int32_t* next_ids, int64_t next_ld) {
+                                                             int32_t* next_ids, int64_t next_ld, int logsm) {
   __shared__ float sh[4];
   __shared__ float bv[4];
   __shared__ int bi[4];
@@ -624,10 +634,11 @@ __global__ void __launch_bounds__(256) argmax_softmax_kernel(const float* __rest
   for (int c = threadIdx.x; c < V; c += 256) se += expf(x[c] - mx);
   se = block_sum(se, sh);
   // argmax over the softmax probabilities, first index on ties (torch.argmax)
-  float best = -1.f;
+  float best = -INFINITY;
   int bidx = 0x7fffffff;
+  const float lse = logf(se);
   for (int c = threadIdx.x; c < V; c += 256) {
-    float p = expf(x[c] - mx) / se;
+    const float p = logsm ? (x[c] - mx) - lse : expf(x[c] - mx) / se;
     if (p > best) {
       best = p;
       bidx = c;
@@ -660,13 +671,13 @@ __global__ void __launch_bounds__(256) argmax_softmax_kernel(const float* __rest
   }
 }
 void argmax_softmax(const float* logits, int B, int V, int64_t* ids_out, int64_t ids_ld, int col, int32_t* next_ids,
-                    int64_t next_ld, hipStream_t s) {
-  argmax_softmax_kernel<<<B, 256, 0, s>>>(logits, V, ids_out, ids_ld, col, next_ids, next_ld);
+                    int64_t next_ld, hipStream_t s, int logsm) {
+  argmax_softmax_kernel<<<B, 256, 0, s>>>(logits, V, ids_out, ids_ld, col, next_ids, next_ld, logsm);
   CAPGEN_HIP(hipGetLastError());
 }
 
 __global__ void __launch_bounds__(256) softmax_rows_kernel(const float* __restrict__ logits, int V,
-                                                           float* __restrict__ probs) {
+                                                           float* __restrict__ probs, int logsm) {
   __shared__ float sh[4];
   const int b = blockIdx.x;
   const float* x = logits + (int64_t)b * V;
@@ -677,10 +688,15 @@ __global__ void __launch_bounds__(256) softmax_rows_kernel(const float* __restri
   float se = 0.f;
   for (int c = threadIdx.x; c < V; c += 256) se += expf(x[c] - mx);
   se = block_sum(se, sh);
-  for (int c = threadIdx.x; c < V; c += 256) y[c] = expf(x[c] - mx) / se;
+  if (logsm) {  // LogSoftmax (model_RL.py:72): (x - max) - log(sum exp)
+    const float lse = logf(se);
+    for (int c = threadIdx.x; c < V; c += 256) y[c] = (x[c] - mx) - lse;
+  } else {
+    for (int c = threadIdx.x; c < V; c += 256) y[c] = expf(x[c] - mx) / se;
+  }
 }
-void softmax_rows(const float* logits, int B, int V, float* probs, hipStream_t s) {
-  softmax_rows_kernel<<<B, 256, 0, s>>>(logits, V, probs);
+void softmax_rows(const float* logits, int B, int V, float* probs, hipStream_t s, int logsm) {
+  softmax_rows_kernel<<<B, 256, 0, s>>>(logits, V, probs, logsm);
   CAPGEN_HIP(hipGetLastError());
 }
 

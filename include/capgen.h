@@ -88,6 +88,9 @@ int capgen_destroy(capgen_t* h);
 int capgen_get_params(capgen_t* h, float* host_dst, int64_t n);
 int capgen_set_params(capgen_t* h, const float* host_src, int64_t n);  /* also resets nothing else */
 int capgen_get_grads(capgen_t* h, float* host_dst, int64_t n);
+/* Overwrite the gradient arena (e.g. gradients reduced outside the engine), then capgen_adam_step
+ * applies them: the host side of a custom data-parallel reduction. */
+int capgen_set_grads(capgen_t* h, const float* host_src, int64_t n);
 /* Adam state: step count and exp_avg / exp_avg_sq arenas (optional checkpoint interop). */
 int capgen_get_adam_state(capgen_t* h, int64_t* step, float* exp_avg, float* exp_avg_sq, int64_t n);
 int capgen_set_adam_state(capgen_t* h, int64_t step, const float* exp_avg, const float* exp_avg_sq, int64_t n);
@@ -126,6 +129,11 @@ int capgen_greedy(capgen_t* h, const void* feats, int feats_dtype, const float* 
 /* Transformer.beam_search (model.py:135-200): ids_out [B, max_length] int64 device. */
 int capgen_beam(capgen_t* h, const void* feats, int feats_dtype, const float* pos, int B, int N, int beam_size,
                 int64_t* ids_out, void* stream);
+
+/* Decode scoring of capgen_greedy / capgen_beam: 0 (default) = Transformer (argmax of Softmax,
+ * beams accumulate probabilities, model.py:124-128,183); 1 = PolicyNetwork, the SCST model
+ * (argmax of LogSoftmax, beams accumulate log-probabilities, model_RL.py:72,126-127,157,182). */
+int capgen_set_decode_log_softmax(capgen_t* h, int enable);
 
 /* Reset the device-side dropout RNG state (test hook: replays a dropout mask). */
 int capgen_set_rng_seed(capgen_t* h, uint64_t seed);
@@ -203,7 +211,10 @@ int capgen_debug_attention(int dtype, int B, int H, int Lq, int Lk, int dk, cons
  * capgen_dp_init, which also broadcasts rank 0's parameters. */
 int capgen_dp_unique_id(char out[128]);
 int capgen_dp_init(capgen_t* h, const char id[128], int rank, int world);
-/* Override the global non-pad target count used by the CE mean (<= 0: all-reduce it). */
+/* Override the global non-pad target count used by the CE mean (<= 0: all-reduce it).  Waits for
+ * the previous step's copy of the override (no race with an in-flight step).  Under DP every rank's
+ * loss output is the GLOBAL mean (Focal) loss: the per-rank partial CE sums are all-reduced before
+ * the FocalLoss transform and the gradient scale (model.py:73-76, loss.py:20-28). */
 int capgen_dp_set_global_count(capgen_t* h, float count);
 
 #ifdef __cplusplus

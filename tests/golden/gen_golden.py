@@ -12,7 +12,8 @@ imported by core/utils.py:7), loads the deterministic fixture weights
   * per-parameter gradient sums / abs-sums / sampled values after loss.backward(),
   * the loss after a second Adam(lr) step and per-parameter deltas after two steps
     (models.py:111-126),
-  * greedy ids + attention_list (model.py:101-132) and beam-5 ids (model.py:135-200).
+  * greedy ids + attention_list (model.py:101-132) and beam-5 ids (model.py:135-200);
+  * PolicyNetwork greedy / beam ids (model_RL.py:100-199: log-softmax scoring).
 Only inputs and outputs are written (tests/golden/*.npz); the reference source never
 leaves this container.
 """
@@ -249,6 +250,59 @@ def make_rl_fixture(tag, cfg, B, N, T, seed, min_valid=None, pad_frac=0.0):
           f"struct={out['structure_loss']:.6f}")
 
 
+def build_policy(PolicyNetwork, cfg):
+    return PolicyNetwork(
+        num_vocab=cfg.num_vocab, max_length=cfg.max_length, encode_dim_positions=cfg.encode_dim_positions,
+        encode_dim_features=cfg.encode_dim_features, device="cpu", pad_idx=cfg.pad_idx, dropout=cfg.dropout,
+        encode_mask=cfg.encode_mask, encode_input_size=cfg.encode_input_size, encode_q_k_dim=cfg.encode_q_k_dim,
+        encode_v_dim=cfg.encode_v_dim, encode_hidden_size=cfg.encode_hidden_size,
+        encode_num_blocks=cfg.encode_num_blocks, encode_num_heads=cfg.encode_num_heads,
+        dim_word_embedding=cfg.dim_word_embedding, decode_input_size=cfg.decode_input_size,
+        decode_q_k_dim=cfg.decode_q_k_dim, decode_v_dim=cfg.decode_v_dim,
+        decode_hidden_size=cfg.decode_hidden_size, decode_num_blocks=cfg.decode_num_blocks,
+        decode_num_heads=cfg.decode_num_heads)
+
+
+def make_policy_decode_fixture(tag, cfg, B, N, T, seed, beam_k, min_valid=None):
+    """PolicyNetwork decoding (model_RL.py:100-199): greedy = argmax of LogSoftmax, beam search
+    accumulates LOG-probabilities (model_RL.py:72,157,182) -- unlike Transformer.beam_search,
+    which adds probabilities.  Also records Transformer.beam_search on the same weights/inputs,
+    so the fixture shows the two rules choosing different beams."""
+    Transformer = import_reference()
+    from core.TRANSFORMER.model_RL import PolicyNetwork
+    torch.manual_seed(0)
+    model = build_policy(PolicyNetwork, cfg)
+    sd = {k: torch.from_numpy(v) for k, v in fixture_state_dict(cfg, seed=seed).items()}
+    model.load_state_dict(sd, strict=True)
+    model.eval()
+    feats, pos, caps = synthetic_batch(B, N, cfg.encode_dim_features, cfg.encode_dim_positions,
+                                       T, cfg.num_vocab, seed=seed + 100, min_valid=min_valid)
+    out = {"feats": feats.numpy(), "pos": pos.numpy(), "caps": caps.numpy()}
+    ids, attn = model.generate_caption_vector(object_features=feats, position_features=pos)
+    out["greedy_ids"] = ids.numpy()
+    out["greedy_attn"] = np.stack(attn).astype(np.float32)
+    out["beam_ids"] = model.beam_search(object_features=feats, position_features=pos, beam_size=beam_k).numpy()
+    out["beam_k"] = np.int64(beam_k)
+    tr = build(Transformer, cfg)
+    tr.load_state_dict(sd, strict=True)
+    tr.eval()
+    out["transformer_beam_ids"] = tr.beam_search(object_features=feats, position_features=pos,
+                                                 beam_size=beam_k).numpy()
+    out["seed"] = np.int64(seed)
+    out["cfg"] = np.array(repr(cfg))
+    path = os.path.join(HERE, f"{tag}.npz")
+    np.savez_compressed(path, **out)
+    ndiff = int((out["beam_ids"] != out["transformer_beam_ids"]).any(1).sum())
+    print(f"wrote {path}: {ndiff}/{B} images decode differently under the Transformer (probability) beam")
+
+
+POLICY_FIXTURES = {
+    # tag: (cfg, B, N, T, seed, beam_k, min_valid)
+    "c1_policy": (preset("C1"), 8, 8, 10, 9, 5, 4),
+    "c2s_policy": (preset("C2", num_vocab=1000), 2, 36, 20, 10, 5, 12),
+}
+
+
 RL_FIXTURES = {
     # tag: (cfg, B, N, T, seed, min_valid, pad_frac)
     "c5_rl": (preset("C1"), 8, 8, 10, 5, 4, 0.0),
@@ -274,6 +328,10 @@ def main(tags=None):
         if tags and tag not in tags:
             continue
         make_fixture(tag, cfg, B, N, T, seed, beam_k=k, min_valid=mv)
+    for tag, (cfg, B, N, T, seed, k, mv) in POLICY_FIXTURES.items():
+        if tags and tag not in tags:
+            continue
+        make_policy_decode_fixture(tag, cfg, B, N, T, seed, k, min_valid=mv)
     for tag, (cfg, B, N, T, seed, mv, pf) in RL_FIXTURES.items():
         if tags and tag not in tags:
             continue

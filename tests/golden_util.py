@@ -17,6 +17,9 @@ FIXTURE_CFG = {
     "c1_splitpos": (lambda: preset("C1", split_position=True), 4),
     "c1_imgobj": (lambda: preset("C1", split_image_objects=True), 7),
     "c1_movefirst": (lambda: preset("C1", move_first_image_feature=True), 8),
+    # POLICY_FIXTURES (PolicyNetwork decoding, log-softmax scoring)
+    "c1_policy": (lambda: preset("C1"), 9),
+    "c2s_policy": (lambda: preset("C2", num_vocab=1000), 10),
     # RL_FIXTURES (SCST, injected rewards)
     "c5_rl": (lambda: preset("C1"), 5),
     "c5_rl_pad": (lambda: preset("C1"), 6),

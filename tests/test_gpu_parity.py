@@ -159,6 +159,67 @@ def test_dp_world1_rccl_train_step_fp32(graph):
     _params_close(a, b, 1e-6)
 
 
+def test_dp_exact_global_mean_two_half_batch_engines_fp32():
+    """SURVEY §8(e) exact-mean rule through the engine's DP path on one GPU: two world-1 RCCL
+    engines each run HALF of the batch with capgen_dp_set_global_count(global non-pad count)
+    (engine.hip forward: count override, per-bucket all-reduce, partial-CE all-reduce).  Their
+    losses and fp32 gradients sum to the full-batch engine's (model.py:76 divides by the GLOBAL
+    count; averaging per-rank means would not match), and one Adam step on the summed gradients
+    gives the full-batch engine's parameters."""
+    from capgen.engine import Engine
+    cfg, seed, z = load_fixture("c1")
+    f, p, c = _inputs(z)
+    full, a, b = (_engine(cfg, seed) for _ in range(3))
+    for e in (full, a, b):
+        e.set_training(False)
+    a.dp_init(Engine.dp_unique_id(), 0, 1)
+    b.dp_init(Engine.dp_unique_id(), 0, 1)
+    n = int((c[:, 1:] != cfg.pad_idx).sum().item())
+    h = c.shape[0] // 2
+    # the override is applied per step: set twice (the second write waits for the first copy)
+    for _ in range(2):
+        for e in (a, b):
+            e.dp_set_global_count(float(n))
+        lf = full.forward(f, p, c).item()
+        la = a.forward(f[:h], p[:h], c[:h]).item()
+        lb = b.forward(f[h:], p[h:], c[h:]).item()
+        assert abs((la + lb) - lf) <= 1e-5 * abs(lf), (la, lb, lf)
+    # the non-pad counts of the halves differ, so per-half means would NOT sum to lf
+    na = int((c[:h, 1:] != cfg.pad_idx).sum().item())
+    assert abs(la * n / na + lb * n / (n - na) - 2 * lf) > 1e-4 or na * 2 == n
+    full.backward()
+    a.backward()
+    b.backward()
+    gf, ga, gb = full.grads_arena(), a.grads_arena(), b.grads_arena()
+    scale = np.abs(gf).max()
+    np.testing.assert_allclose(ga + gb, gf, atol=1e-5 * scale, rtol=0)
+    a.set_grads_arena(gf)   # what the all-reduce would leave on every rank (to summation order)
+    a.adam_step()
+    full.adam_step()
+    _params_close(a, full, 1e-6)
+
+
+@pytest.mark.parametrize("tag", ["c1", "c1_focal"])
+def test_dp_world1_loss_path_equals_single_process_fp32(tag):
+    """The DP loss path (per-rank partial CE, 4-byte all-reduce, then CE mean / FocalLoss and the
+    gradient scale from the global mean CE) at world size 1 equals the single-process loss and
+    gradients, FocalLoss included (round 1 refused FocalLoss under DP)."""
+    from capgen.engine import Engine
+    cfg, seed, z = load_fixture(tag)
+    f, p, c = _inputs(z)
+    a, b = _engine(cfg, seed), _engine(cfg, seed)
+    for e in (a, b):
+        e.set_training(False)
+    a.dp_init(Engine.dp_unique_id(), 0, 1)
+    la = a.forward(f, p, c).item()
+    lb = b.forward(f, p, c).item()
+    assert abs(la - float(z["loss"])) < 1e-3 and abs(la - lb) <= 1e-6 * abs(lb), (la, lb, float(z["loss"]))
+    a.backward()
+    b.backward()
+    ga, gb = a.grads_arena(), b.grads_arena()
+    np.testing.assert_allclose(ga, gb, atol=1e-6 * np.abs(gb).max(), rtol=0)
+
+
 @pytest.mark.parametrize("tag", ["c1", "c1_encmask", "c2s", "c1_imgobj", "c1_movefirst"])
 def test_greedy_bit_exact(tag):
     cfg, seed, z = load_fixture(tag)
@@ -168,6 +229,38 @@ def test_greedy_bit_exact(tag):
     ids, attn = e.greedy(f, p)
     np.testing.assert_array_equal(ids.cpu().numpy(), z["greedy_ids"])
     np.testing.assert_allclose(attn.cpu().numpy(), z["greedy_attn"], atol=1e-4)
+
+
+@pytest.mark.parametrize("tag", ["c1_policy", "c2s_policy"])
+def test_policy_network_decode_matches_reference(tag):
+    """PolicyNetwork.generate_caption_vector / beam_search (model_RL.py:100-199: LogSoftmax
+    scoring, beams accumulate log-probabilities) vs the reference's own outputs (fixtures made by
+    gen_golden.py), through capgen.model.PolicyNetwork and SelfCriticNetwork.generate_caption's
+    dispatch; the Transformer (probability) beam on the same engine reproduces the fixture's
+    transformer_beam_ids, which differ on c1_policy."""
+    import warnings
+    from capgen.model import PolicyNetwork
+    from capgen.models import SelfCriticNetwork
+    cfg, seed, z = load_fixture(tag)
+    sd = {k: torch.from_numpy(v) for k, v in fixture_state_dict(cfg, seed=seed, with_buffer=False).items()}
+    m = PolicyNetwork.from_config(cfg.replace(dtype="fp32"), DEV, state_dict=sd)
+    m.eval()
+    f, p, _ = _inputs(z)
+    ids, attn = m.generate_caption_vector(f, p)
+    np.testing.assert_array_equal(ids.cpu().numpy(), z["greedy_ids"])
+    np.testing.assert_allclose(np.stack(attn), z["greedy_attn"], atol=1e-4)
+    k = int(z["beam_k"])
+    np.testing.assert_array_equal(m.beam_search(f, p, beam_size=k).cpu().numpy(), z["beam_ids"])
+    m.engine.set_decode_log_softmax(False)
+    np.testing.assert_array_equal(m.beam_search(f, p, beam_size=k).cpu().numpy(), z["transformer_beam_ids"])
+    w2i = {"<NULL>": 0, "<START>": 1, "<END>": 2}
+    w2i.update({f"w{i}": i for i in range(3, cfg.num_vocab)})
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        scn = SelfCriticNetwork(cfg.replace(dtype="fp32"), word_to_idx=w2i, device=DEV, state_dict=sd)
+    scn.model.eval()
+    caps, _ = scn.generate_caption(f, p, beam_size=k)
+    assert caps == scn.decode_captions(z["beam_ids"])
 
 
 @pytest.mark.parametrize("tag", ["c1", "c1_encmask", "c2s", "c1_imgobj", "c1_movefirst"])
@@ -725,3 +818,100 @@ def test_decode_graph_replay_matches_eager(tag, monkeypatch):
                 e.forward(f, p, c)
                 e.backward()
                 e.adam_step()
+
+
+# ---- the benchmarked configuration itself (C2: B=64, N=36, F=2048, T=20, V=10000, 6+6 blocks) ----
+def _c2_setup(B=64, dtype="fp32", dropout=None, weights="init"):
+    import sys, os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle import capgen_oracle as O
+    from capgen.config import preset
+    from capgen.engine import Engine
+    from capgen.params import reference_init_state_dict
+    from capgen.synthetic import synthetic_batch
+    cfg = preset("C2")
+    if dropout is not None:
+        cfg = cfg.replace(dropout=dropout)
+    f, p, c = synthetic_batch(B, 36, cfg.encode_dim_features, cfg.encode_dim_positions, 20, cfg.num_vocab,
+                              seed=1000)   # bench.py's rank-0 batch
+    # bench.py's weights, or the fixtures' closed-form ones (peaked softmaxes: the random-init model is
+    # nearly uniform over 10000 words, where the probability-sum beam meets exact near-ties)
+    sd = (reference_init_state_dict(cfg, seed=0, with_buffer=False) if weights == "init"
+          else fixture_state_dict(cfg, seed=0, with_buffer=False))
+    e = Engine(cfg.replace(dtype=dtype), DEV)
+    e.load_state_dict(sd)
+    return O, cfg, sd, e, f, p, c
+
+
+def test_c2_full_size_fp32_matches_oracle():
+    """The exact shapes bench.py times (model.py:79-98 at C2), fp32 parity mode, eval: loss and
+    every logit within 1e-3 of the CPU oracle (north star), every gradient's abs-sum within 1e-3
+    relative (the autotuned split-K fp32 GEMMs, the 10000-wide CE, 2304-row encoder)."""
+    O, cfg, sd, e, f, p, c = _c2_setup()
+    e.set_training(False)
+    loss = e.forward(f.to(DEV), p.to(DEV), c.to(DEV)).item()
+    lg = e.logits(64, 20).cpu()
+    e.backward()
+    g = e.grads_state_dict()
+    P = O.make_params(sd)
+    lo, lgo = O.forward_loss(P, cfg, f, p, c, training=False)
+    assert abs(loss - lo.item()) < 1e-3, (loss, lo.item())
+    assert (lg - lgo.detach()).abs().max().item() < 1e-3
+    lo.backward()
+    for n, t in P.items():
+        ref = t.grad.double().abs().sum().item()
+        got = g[n].double().abs().sum().item()
+        assert abs(got - ref) <= 1e-3 * ref + 1e-6, (n, got, ref)
+
+
+def test_c2_full_size_bf16_train_mode_close_to_fp32():
+    """bench.py's path (bf16 MFMA GEMMs with split-K, MFMA attention, dropout 0.3 / 0.1) at C2
+    vs the fp32 parity path with the same counter-RNG dropout masks: loss within 1 % and every
+    gradient within 10 % relative L2 (bf16 activations through 12 blocks; measured worst ~4 %),
+    then five bucketed train steps whose losses track the fp32 engine's within 1 %."""
+    _, cfg, sd, e16, f, p, c = _c2_setup(dtype="bf16", dropout=0.3)
+    _, _, _, e32, _, _, _ = _c2_setup(dtype="fp32", dropout=0.3)
+    fd, pd, cd = f.to(DEV), p.to(DEV), c.to(DEV)
+    for e in (e16, e32):
+        e.set_training(True)
+        e.set_rng_seed(99)
+    l16 = e16.forward(fd.bfloat16(), pd, cd).item()
+    l32 = e32.forward(fd, pd, cd).item()
+    assert abs(l16 - l32) < 1e-2 * abs(l32), (l16, l32)
+    e16.backward()
+    e32.backward()
+    g16, g32 = e16.grads_state_dict(), e32.grads_state_dict()
+    worst = max((((g16[n].double() - g32[n].double()).norm() / (g32[n].double().norm() + 1e-12)).item(), n)
+                for n in g32)
+    assert worst[0] < 0.1, worst
+    for i in range(5):
+        a = e16.train_step(fd.bfloat16(), pd, cd).item()
+        b = e32.train_step(fd, pd, cd).item()
+        assert abs(a - b) < 1e-2 * abs(b), (i, a, b)
+
+
+@pytest.mark.parametrize("weights", ["init", "fixture"])
+def test_c2_full_size_greedy_fp32_matches_oracle(weights):
+    """Greedy ids bit-exact at B=64 vs the oracle at the C2 model (V=10000), fp32 parity mode
+    (model.py:101-132), with bench.py's random-init weights and with the fixture weights."""
+    O, cfg, sd, e, f, p, c = _c2_setup(weights=weights)
+    e.set_training(False)
+    P = O.make_params(sd, requires_grad=False)
+    ids, attn = e.greedy(f.to(DEV), p.to(DEV))
+    ref, attn_ref = O.greedy(P, cfg, f, p)
+    np.testing.assert_array_equal(ids.cpu().numpy(), ref.numpy())
+    np.testing.assert_allclose(attn.cpu().numpy(), np.stack(attn_ref), atol=1e-4)
+
+
+def test_c2_full_size_beam_fp32_matches_oracle():
+    """Beam-5 ids exact at B=16 vs the oracle at the C2 model (V=10000), fp32 parity mode
+    (model.py:135-200), fixture weights; and the PolicyNetwork (log-probability) beam."""
+    O, cfg, sd, e, f, p, c = _c2_setup(weights="fixture")
+    e.set_training(False)
+    P = O.make_params(sd, requires_grad=False)
+    b = 16
+    ids5 = e.beam(f[:b].to(DEV), p[:b].to(DEV), 5)
+    np.testing.assert_array_equal(ids5.cpu().numpy(), O.beam(P, cfg, f[:b], p[:b], 5).numpy())
+    e.set_decode_log_softmax(True)
+    ids5 = e.beam(f[:b].to(DEV), p[:b].to(DEV), 5)
+    np.testing.assert_array_equal(ids5.cpu().numpy(), O.beam(P, cfg, f[:b], p[:b], 5, log_softmax=True).numpy())

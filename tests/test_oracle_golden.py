@@ -64,6 +64,23 @@ def test_greedy_and_beam(tag):
     np.testing.assert_array_equal(O.beam(P, cfg, f, p, k).numpy(), z["beam_ids"])
 
 
+@pytest.mark.parametrize("tag", ["c1_policy", "c2s_policy"])
+def test_policy_network_greedy_and_beam(tag):
+    """PolicyNetwork decoding (model_RL.py:100-199, log-softmax scoring) vs the reference's own
+    output; c1_policy also differs from the Transformer's probability beam on some images."""
+    cfg, seed, z = load_fixture(tag)
+    P = O.make_params(fixture_state_dict(cfg, seed=seed, with_buffer=False), requires_grad=False)
+    f, p = (torch.from_numpy(z[k]) for k in ("feats", "pos"))
+    ids, attn = O.greedy(P, cfg, f, p, log_softmax=True)
+    np.testing.assert_array_equal(ids.numpy(), z["greedy_ids"])
+    np.testing.assert_allclose(np.stack(attn), z["greedy_attn"], atol=1e-5)
+    k = int(z["beam_k"])
+    np.testing.assert_array_equal(O.beam(P, cfg, f, p, k, log_softmax=True).numpy(), z["beam_ids"])
+    np.testing.assert_array_equal(O.beam(P, cfg, f, p, k).numpy(), z["transformer_beam_ids"])
+    if tag == "c1_policy":
+        assert (z["beam_ids"] != z["transformer_beam_ids"]).any()
+
+
 def test_sinusoid_table_matches_oracle():
     np.testing.assert_array_equal(sinusoid_table(19, 512), O.sinusoid_table(19, 512).numpy())
 
