@@ -73,9 +73,12 @@ def dominant_gemm(eng, steps=50):
 
 
 def _pmc_traffic():
-    """HBM bytes per train step from the committed rocprofv3 PMC passes (FETCH_SIZE x2 per the
-    gfx950 correction + WRITE_SIZE, summed over one step's kernels; tools/pmcsum.py)."""
-    path = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
+    """HBM bytes per train step from the COMMITTED rocprofv3 PMC passes (FETCH_SIZE x2 per the
+    gfx950 correction + WRITE_SIZE, summed over one step's kernels; tools/pmcsum.py) -- a file
+    measured on this code by tools/round_profile.sh, not in this run (PMC needs its own passes)."""
+    path = os.path.join(REPO, "profiles", "r02_pmc_traffic.json")
+    if not os.path.exists(path):
+        path = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
     if not os.path.exists(path):
         return None
     with open(path) as fh:
@@ -83,26 +86,37 @@ def _pmc_traffic():
     return {"bytes_per_step": d["hbm_bytes_per_step"], "source": os.path.relpath(path, REPO)}
 
 
-def cpu_baseline(cfg, steps=3, warmup=1):
+def cpu_baseline(cfg, steps=5, warmup=2, c1_steps=50):
     """The pinned CPU oracle (fp32 eager torch, train mode = dropout on) on this host's cores:
-    a bounded sample of the same workload (same B/N/T/model), time per step -> images/s."""
+    a bounded sample of the same workload (same B/N/T/model) -> images/s, SURVEY §8(d): 2 warm-up +
+    5 timed steps at C2 (the reported value) and 2 + 50 at C1 (reported beside it).  Threads: torch's
+    intra-op pool as configured for this box (OMP_NUM_THREADS; os.cpu_count() reports the whole host,
+    of which one GPU box owns a share)."""
     sys.path.insert(0, REPO)
     from oracle import capgen_oracle as O
+    from capgen import preset
     from capgen.params import reference_init_state_dict
     from capgen.synthetic import synthetic_batch
     threads = torch.get_num_threads()
-    f, p, c = synthetic_batch(B, N, cfg.encode_dim_features, cfg.encode_dim_positions, T, cfg.num_vocab, seed=1000)
-    P = O.make_params(reference_init_state_dict(cfg.replace(dtype="fp32"), seed=0))
-    opt = O.make_adam(P, cfg)
-    for _ in range(warmup):
-        O.train_step(P, opt, cfg, f, p, c, training=True)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        O.train_step(P, opt, cfg, f, p, c, training=True)
-    dt = (time.perf_counter() - t0) / steps
+
+    def time_steps(c, b, n, t, warm, timed):
+        f, p, cap = synthetic_batch(b, n, c.encode_dim_features, c.encode_dim_positions, t, c.num_vocab, seed=1000)
+        P = O.make_params(reference_init_state_dict(c.replace(dtype="fp32"), seed=0))
+        opt = O.make_adam(P, c)
+        for _ in range(warm):
+            O.train_step(P, opt, c, f, p, cap, training=True)
+        t0 = time.perf_counter()
+        for _ in range(timed):
+            O.train_step(P, opt, c, f, p, cap, training=True)
+        return (time.perf_counter() - t0) / timed
+
+    dt = time_steps(cfg, B, N, T, warmup, steps)
+    c1 = preset("C1", dropout=0.3)
+    dt1 = time_steps(c1, 8, 8, 10, warmup, c1_steps)
     return {"value": round(B / dt, 2), "unit": "images/s", "cores": threads, "kind": "port",
             "sample": f"{warmup} warm-up + {steps} timed C2 train steps (B={B}, fp32 eager torch CPU, dropout on), "
-                      f"{dt:.3f} s/step"}
+                      f"{dt:.3f} s/step; C1 (B=8): {warmup} + {c1_steps} steps, {dt1 * 1e3:.1f} ms/step",
+            "c1_value": round(8 / dt1, 1)}
 
 
 def main():
@@ -113,7 +127,7 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--graph", action="store_true", help="replay the step as one hipGraph (slower on ROCm 7)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-steps", type=int, default=5)
     args = ap.parse_args()
 
     from capgen import preset
@@ -195,7 +209,8 @@ def main():
                      "traffic": traffic["bytes_per_step"] if traffic else None,
                      "scope": f"one train step = {B} images x {gfl_img:.5f} GFLOP/image "
                               f"algorithmic (SURVEY §8(d)); step time {step_ms_events:.4f} ms from HIP events "
-                              f"on the launch stream" + (f"; traffic = HBM bytes/step from {traffic['source']}"
+                              f"on the launch stream" + (f"; traffic = HBM bytes/step from the committed PMC "
+                                                         f"summary {traffic['source']} (not measured in this run)"
                                                          if traffic else "")},
         "final_loss": round(final_loss, 5),
     }

@@ -1252,9 +1252,24 @@ struct capgen_engine {
         CAPGEN_HIP(hipGraphDestroy(graph));
         fkey = k;
       }
+      static const bool host_timing = std::getenv("CAPGEN_HOST_TIMING") != nullptr;  // diagnostic
+      static double tb = 0, tl = 0;
+      static int nsteps = 0;
+      auto t0 = std::chrono::steady_clock::now();
       CAPGEN_HIP(hipGraphLaunch(fexec, es));
+      auto t1 = std::chrono::steady_clock::now();
       fB = B, fN = N, fT = T, fwd_drop = training;  // host state forward() would have set
       backward(es, /*step_params=*/true);
+      if (host_timing) {
+        auto t2 = std::chrono::steady_clock::now();
+        tl += std::chrono::duration<double, std::micro>(t1 - t0).count();
+        tb += std::chrono::duration<double, std::micro>(t2 - t1).count();
+        if (++nsteps % 20 == 0) {
+          std::fprintf(stderr, "[capgen host] per step: forward graph launch %.1f us, backward enqueue %.1f us\n",
+                       tl / 20, tb / 20);
+          tl = tb = 0;
+        }
+      }
     } else if (!graph_on) {
       body();
     } else {

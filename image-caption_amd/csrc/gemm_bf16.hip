@@ -70,27 +70,62 @@ struct Op {
   static constexpr int NI = BYTES / 1024;       // 1-KB DMA instructions per stage
   static constexpr int PER_WAVE = NI / NW;
   static_assert(PER_WAVE >= 1 && NI % NW == 0, "tile too small for the wave count");
+  static constexpr uint32_t OOB = 0x80000000u;  // past any buffer: the DMA lands zeros
 
-  // issue this wave's share of the LDS-DMA for one K tile
-  static __device__ __forceinline__ void issue(const bf16* __restrict__ src, int64_t ld, int r0, int R, int k0,
-                                               int K, char* img, int wave, int lane, const void* zero) {
+  // The operand is read through a buffer resource (bounds-checked: an offset past num_records
+  // returns zeros), so the k-loop issues each 1-KB piece with NO per-piece address arithmetic:
+  // every lane's byte offset is fixed for the tile (voff, set up once) and the k-tile advance is
+  // one scalar soffset (kstep per tile).  Rows past the tile's extent read past num_records
+  // (non-TRANS: rows >= R; TRANS: k rows >= K); a chunk past the minor extent (TRANS: columns
+  // >= R) gets the OOB offset once; only a non-TRANS K tail needs a per-tile lane mask.
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint32_t voff[PER_WAVE];
+  int kch[PER_WAVE];  // non-TRANS: k offset of the lane's chunk inside the tile
+  uint32_t kstep;
+
+  __device__ __forceinline__ void setup(const bf16* src, int64_t ld, int r0, int R, int K, int kt_first, int wave,
+                                        int lane) {
+    const int64_t rows = TRANS ? K : R;
+    rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(src), 0, (int)(rows * ld * 2), 0x00020000);
+    kstep = TRANS ? (uint32_t)(BK * ld * 2) : (uint32_t)(BK * 2);
 #pragma unroll
     for (int j = 0; j < PER_WAVE; ++j) {
       const int i = wave + NW * j;
       const int b = i * 1024 + lane * 16;
-      const bf16* p;
-      bool ok;
       if constexpr (!TRANS) {
         const int row = b >> 7, ch = swz_k(row, (b >> 4) & 7);
-        ok = (r0 + row < R) && (k0 + ch * 8 < K);
-        p = src + (int64_t)(r0 + row) * ld + (k0 + ch * 8);
+        kch[j] = ch * 8;
+        voff[j] = r0 + row < R ? (uint32_t)(((int64_t)(r0 + row) * ld + (int64_t)kt_first * BK + ch * 8) * 2) : OOB;
       } else {
         const int k = b / (ROWS * 2), ch = swz_t<ROWS>(k, (b % (ROWS * 2)) >> 4);
-        ok = (k0 + k < K) && (r0 + ch * 8 < R);
-        p = src + (int64_t)(k0 + k) * ld + (r0 + ch * 8);
+        kch[j] = 0;
+        voff[j] = r0 + ch * 8 < R ? (uint32_t)((((int64_t)kt_first * BK + k) * ld + r0 + ch * 8) * 2) : OOB;
       }
-      __builtin_amdgcn_global_load_lds(ok ? (const void*)p : zero, (lds_void*)(img + i * 1024), 16, 0, 0);
     }
+  }
+
+  // this wave's share of the LDS-DMA for k-tile t (relative to kt_first) into the stage image
+  // img; tail: the tile ends past K (kb = its first k)
+  __device__ __forceinline__ void issue(int t, char* img, bool tail, int kb, int K, int wave) const {
+    const uint32_t soff = (uint32_t)t * kstep;
+    if (!TRANS && tail) {  // uniform: the last k-tile of a K that is not a multiple of 64
+#pragma unroll
+      for (int j = 0; j < PER_WAVE; ++j) dma(kb + kch[j] < K ? voff[j] : OOB, soff, img + (wave + NW * j) * 1024);
+    } else {
+#pragma unroll
+      for (int j = 0; j < PER_WAVE; ++j) dma(voff[j], soff, img + (wave + NW * j) * 1024);
+    }
+  }
+
+  // one 1-KB LDS-DMA piece (buffer_load_dwordx4 ... lds: lane l's 16 B land at M0 + 16 l), issued
+  // by inline asm.  With the global_load_lds builtin hipcc treated the in-flight DMA as a pending
+  // write to the staging array and emitted `s_waitcnt vmcnt(0)` before the next ds_read of ANY
+  // stage, draining every prefetch one step early (guide cdna_hip_programming.md §5 item 4(a));
+  // the k-loop retires the DMA itself with counted vmcnt waits + a raw barrier (wait_younger).
+  __device__ __forceinline__ void dma(uint32_t v, uint32_t soff, char* lds) const {
+    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(v), "s"(rsrc), "s"(soff),
+                 "{m0}"((unsigned)(uintptr_t)lds)
+                 : "memory");
   }
 
   // 16-row fragment starting at rb for k-step ks (permuted K order, see header)
@@ -205,35 +240,47 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int mt, int nt, int
   const int per = (nk_all + splitk - 1) / splitk;
   const int kt0 = split * per;
   const int nk = max(0, min(nk_all - kt0, per));  // K tiles of this slice
-  auto issue = [&](int kt) {
-    kt += kt0;
-    char* st = smem + ((kt - kt0) % STAGES) * SB;
-    OA::issue(A, g.lda, m0, g.M, kt * BK, g.K, st, wave, lane, zero);
-    OB::issue(B, g.ldb, n0, g.N, kt * BK, g.K, st + OA::BYTES, wave, lane, zero);
+  OA oa;
+  OB ob;
+  oa.setup(A, g.lda, m0, g.M, g.K, kt0, wave, lane);
+  ob.setup(B, g.ldb, n0, g.N, g.K, kt0, wave, lane);
+  auto issue = [&](int t, char* st) {
+    const int kb = (kt0 + t) * BK;
+    const bool tail = kb + BK > g.K;
+    oa.issue(t, st, tail, kb, g.K, wave);
+    ob.issue(t, st + OA::BYTES, tail, kb, g.K, wave);
   };
 #pragma unroll
   for (int p = 0; p < STAGES - 1; ++p)
-    if (p < nk) issue(p);
+    if (p < nk) issue(p, smem + p * SB);
 
-  for (int kt = 0; kt < nk; ++kt) {
-    // tile kt landed for this wave (up to STAGES-2 younger tiles may still fly) ...
-    static_assert((STAGES - 2) * LPT <= 63, "vmcnt range");
-    wait_younger<LPT, STAGES - 2>(nk - 1 - kt);
-    __builtin_amdgcn_s_barrier();  // ... for every wave; stage (kt-1)%STAGES is free again
-    if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1);
-    const char* st = smem + (kt % STAGES) * SB;
+  // k-loop unrolled by STAGES: tile kb + s lives in stage s, so every LDS offset is a constant
+  // (ds_read immediate offsets, a scalar M0 per DMA piece: no address VALU in the loop)
+  static_assert((STAGES - 2) * LPT <= 63, "vmcnt range");
+  for (int kb = 0; kb < nk; kb += STAGES) {
 #pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      bf16x8 af[FM], bfr[FN];
+    for (int s = 0; s < STAGES; ++s) {
+      const int kt = kb + s;
+      if (kt < nk) {
+        // tile kt landed for this wave (up to STAGES-2 younger tiles may still fly) ...
+        wait_younger<LPT, STAGES - 2>(nk - 1 - kt);
+        __builtin_amdgcn_s_barrier();  // ... for every wave; stage (s-1) % STAGES is free again
+        if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, smem + ((s + STAGES - 1) % STAGES) * SB);
+        const char* st = smem + s * SB;
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = OA::frag(st, wm * TM + i * 16, ks, lane);
+        for (int ks = 0; ks < BK / 32; ++ks) {
+          bf16x8 af[FM], bfr[FN];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = OB::frag(st + OA::BYTES, wn * TN + j * 16, ks, lane);
+          for (int i = 0; i < FM; ++i) af[i] = OA::frag(st, wm * TM + i * 16, ks, lane);
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+          for (int j = 0; j < FN; ++j) bfr[j] = OB::frag(st + OA::BYTES, wn * TN + j * 16, ks, lane);
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        }
+      }
     }
   }
 

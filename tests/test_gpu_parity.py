@@ -361,13 +361,16 @@ def test_train_step_equals_forward_backward_adam_bf16(graph):
         if sa[k].dim() == 2 and k != "decoder.word_embedding.weight":  # every Linear weight
             assert torch.equal(sa[k], sb[k]), k
         torch.testing.assert_close(sa[k], sb[k], atol=1e-5, rtol=0, msg=k)
-    for _ in range(2):  # later steps: losses agree (params drift in the last bits, see above)
+    for _ in range(2):  # later steps: losses agree -- the LayerNorm / bias gradients are f32-atomic
+        # sums (order-dependent in the last bits) and Adam's first steps act like sign(g) * lr, so a
+        # near-zero gradient whose last bits differ moves its parameter by up to 2 lr: measured
+        # loss drift 1.4e-4 relative after three steps; a missed or doubled bucket update is O(1e-2)
         la = a.train_step(f, p, c).clone()
         lb = b.forward(f, p, c).clone()
         b.backward()
         b.adam_step()
         torch.cuda.synchronize()
-        assert abs(la.item() - lb.item()) < 1e-4 * abs(lb.item())
+        assert abs(la.item() - lb.item()) < 1e-3 * abs(lb.item())
 
 
 def test_dropout_backward_directional_derivative_fp32():

@@ -23,9 +23,13 @@ def run(M, N, K, ta=0, tb=0, out_f32=False, reps=20, bias=False, relu=False):
                 C.c_void_p(Cc.data_ptr()), N, 1, 0 if out_f32 else 1, C.c_void_p(b.data_ptr()) if bias else None,
                 1.0, 0, int(relu), C.c_void_p(s.cuda_stream))
     g = torch.cuda.CUDAGraph()
-    _lib.check(lib.capgen_debug_gemm(*args()))
+    global _CS
+    if "_CS" not in globals():
+        _CS = torch.cuda.Stream()
+    with torch.cuda.stream(_CS):  # warm-up on the capture stream: sizes its split-K workspace
+        _lib.check(lib.capgen_debug_gemm(*args()))
     torch.cuda.synchronize()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, stream=_CS):
         for _ in range(reps):
             _lib.check(lib.capgen_debug_gemm(*args()))
     g.replay()
@@ -118,10 +122,35 @@ elif __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "nnnt":
             run(M, N, K, 0, tb, 0)
 elif __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "sweep":
     sweep()
-elif __name__ == "__main__":
+elif __name__ == "__main__" and len(sys.argv) == 1:
     shapes = [(2304, 2048, 512, 0, 0, 0), (2304, 2048, 2048, 0, 0, 0), (2304, 2048, 8192, 0, 0, 0),
               (4096, 4096, 4096, 0, 0, 0), (2304, 6144, 512, 0, 0, 0), (1216, 10000, 512, 0, 0, 1),
               (1216, 512, 512, 0, 1, 0), (2304, 512, 2048, 0, 1, 0), (2048, 512, 2304, 1, 1, 1),
               (512, 512, 2304, 1, 1, 1), (1216, 512, 10000, 0, 1, 0), (512, 2176, 2304, 1, 1, 1)]
     for sh in shapes:
         run(*sh)
+
+
+def matrix(shapes, sks=(1, 2, 4, 8), variants=range(1, 23)):
+    """Every (variant, split-K) on each shape, graph-replayed (device time per launch)."""
+    for sh in shapes:
+        res = []
+        for v in variants:
+            for sk in sks:
+                _lib.check(lib.capgen_debug_gemm_variant(v + 100 * sk))
+                try:
+                    us = run(*sh, reps=20)
+                    res.append((us, v, sk))
+                except RuntimeError as e:
+                    print("  skip", v, sk, e)
+        res.sort()
+        print(f"best for {sh}: " + ", ".join(f"v{v}x{sk} {us:.2f}" for us, v, sk in res[:6]), flush=True)
+    _lib.check(lib.capgen_debug_gemm_variant(0))
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "matrix2":
+    matrix([(1216, 512, 10000, 0, 1, 0), (2304, 512, 6144, 0, 1, 0), (1216, 10000, 512, 0, 0, 1)],
+           variants=(1, 3, 4, 5, 6, 8, 10, 17, 20))
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "matrix":
+    matrix([(2304, 512, 2048, 0, 1, 0), (2304, 2048, 512, 0, 0, 0), (2304, 512, 512, 0, 0, 0),
+            (1216, 512, 2048, 0, 1, 0), (2304, 1536, 512, 0, 0, 0)])
