@@ -8,6 +8,7 @@ namespace capgen {
 // Row (b, i) of head h of a [.., H*dk] activation lives at base + b*bs + i*ld + h*dk.
 struct AttnGeom {
   int B = 0, H = 0, Lq = 0, Lk = 0, dk = 0;
+  int prio = 0;  // 1: raise the waves' issue priority (critical path)
   const void* q = nullptr; int64_t q_ld = 0, q_bs = 0;
   const void* k = nullptr; int64_t k_ld = 0, k_bs = 0;
   const void* v = nullptr; int64_t v_ld = 0, v_bs = 0;

@@ -87,6 +87,7 @@ struct Acts {
   float* logits;
   void* dlogits;
   float *loss_row, *grad_scale, *loss, *loss_ce;
+  float* gEnc32;  // f32 partial sum of the encoder-output gradient over decoder blocks Ld-1 .. 1
   // SCST (rl.hip): per-row sample / lse / logp[sample] / entropy, per-image entropy, scalars
   int32_t* rl_sample;
   float *rl_lse, *rl_logp, *rl_ent, *rl_ent_img, *rl_score, *rl_scal;
@@ -245,6 +246,7 @@ struct capgen_engine {
   hipStream_t ec = nullptr;   // bucket stream: per-bucket gradient all-reduce (RCCL) + Adam
   hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_b1 = nullptr, ev_b2 = nullptr, ev_cj = nullptr;
+  hipEvent_t ev_part = nullptr;  // es2: the encoder-output gradient partials are summed
   float *params = nullptr, *grads = nullptr, *am = nullptr, *av = nullptr;
   bf16* shadow = nullptr;
   float* pe = nullptr;  // [max_length-1, dd] f32 sinusoid table
@@ -325,6 +327,34 @@ struct capgen_engine {
   bool keep_probs(const AttnGeom& g) const { return !(act == DType::BF16 && attention_mfma_ok(g)); }
   static uint32_t site(int dec, int layer, int kind) { return (uint32_t)((dec * 64 + layer) * 16 + kind); }
 
+  // issue priority of a launch: kernels on the critical stream run their waves at s_setprio 3 so
+  // that the weight-gradient / Adam waves of the side streams sharing their CUs yield the issue
+  // slots to them (CAPGEN_PRIO=0 disables)
+  bool prio_on = [] {
+    const char* e = std::getenv("CAPGEN_PRIO");
+    return !(e && e[0] == '0');
+  }();
+  int prio(hipStream_t s) const { return prio_on && s == es && es2 != es ? 1 : 0; }
+
+  // the row / attention kernels with the launch's issue priority (prio above)
+  void lnf(LnFwd l, hipStream_t s) const {
+    l.prio = prio(s);
+    layernorm_fwd(l, act, s);
+  }
+  void lnb(LnBwd l, hipStream_t s) const {
+    l.prio = prio(s);
+    layernorm_bwd(l, act, s);
+  }
+  void attf(AttnGeom g, void* o, float* probs, DType t, hipStream_t s) const {
+    g.prio = prio(s);
+    attention_fwd(g, o, probs, t, s);
+  }
+  void attb(AttnGeom g, const float* probs, const void* dout, void* dq, void* dk, void* dv, DType t,
+            hipStream_t s) const {
+    g.prio = prio(s);
+    attention_bwd(g, probs, dout, dq, dk, dv, t, s);
+  }
+
   // C[M,N] = A[M,K] . W[N,K]^T  (nn.Linear)
   void linear(const void* X, int64_t ldx, int64_t woff, int64_t ldw, void* C, int64_t ldc, DType tout, int M,
               int N, int K, const float* bias, int relu, hipStream_t s) {
@@ -332,6 +362,7 @@ struct capgen_engine {
     ga.M = M, ga.N = N, ga.K = K, ga.A = X, ga.lda = ldx, ga.B = W(woff), ga.ldb = ldw, ga.C = C, ga.ldc = ldc;
     ga.bias = bias;
     ga.relu = relu;
+    ga.prio = prio(s);
     gemm(ga, act, tout, false, false, s);
   }
   // C = X . W^T into ln.a, then y = LayerNorm(drop(C + bias) + res (+ pe)) (modules.py:86-90).
@@ -340,7 +371,7 @@ struct capgen_engine {
   void linear_ln(const void* X, int64_t ldx, int64_t woff, int64_t ldw, int M, int N, int K, const LnFwd& ln,
                  hipStream_t s) {
     linear(X, ldx, woff, ldw, const_cast<void*>(ln.a), N, act, M, N, K, nullptr, 0, s);
-    layernorm_fwd(ln, act, s);
+    lnf(ln, s);
   }
   // a LayerNorm backward descriptor (striped accumulators); b_off < 0: no producing-Linear bias
   LnBwd lnb_desc(int M, int d, const void* dy, const void* v, const float* mean, const float* rstd, int64_t lng,
@@ -364,6 +395,7 @@ struct capgen_engine {
     ga.aux = relu_aux;
     ga.ldaux = ldx;
     ga.alpha_ptr = alpha_ptr;
+    ga.prio = prio(s);
     gemm(ga, act, act, false, true, s);
   }
   // dW[N,K] = alpha * dY[M,N]^T . X[M,K]   (f32, overwrites)
@@ -372,6 +404,7 @@ struct capgen_engine {
     GemmArgs ga;
     ga.M = N, ga.N = K, ga.K = M, ga.A = dY, ga.lda = ldy, ga.B = X, ga.ldb = ldx, ga.C = G(goff), ga.ldc = ldg;
     ga.alpha_ptr = alpha_ptr;
+    ga.prio = prio(s);
     gemm(ga, act, DType::F32, true, true, s);
   }
 
@@ -439,6 +472,7 @@ struct capgen_engine {
     p.take(a.grad_scale, 4);
     p.take(a.loss, 4);
     p.take(a.loss_ce, 4);
+    p.take(a.gEnc32, (size_t)Me * d);
     p.take(a.rl_sample, Md);
     p.take(a.rl_lse, Md);
     p.take(a.rl_logp, Md);
@@ -637,7 +671,7 @@ struct capgen_engine {
     if (valid) g.key_valid = valid, g.kv_bs = N, g.causal = 1;
     g.temperature = std::sqrt((float)dke);
     g.drop = mk_drop(pa, site(0, layer, 0), drop_on);
-    attention_fwd(g, A.att, keep_probs(g) ? A.P : nullptr, act, s);
+    attf(g, A.att, keep_probs(g) ? A.P : nullptr, act, s);
     LnFwd l1;
     l1.M = Me, l1.d = d, l1.a = a.tmp, l1.drop = mk_drop(p, site(0, layer, 1), drop_on), l1.res = X;
     l1.gamma = P(w.ln1g), l1.beta = P(w.ln1b), l1.y = A.Y, l1.v_save = A.v1, l1.mean = A.m1, l1.rstd = A.r1;
@@ -668,7 +702,7 @@ struct capgen_engine {
     LnFwd l2;
     l2.M = Me, l2.d = d, l2.a = a.tmp, l2.gamma = P(L.enc_lng), l2.beta = P(L.enc_lnb);
     l2.y = a.X[0], l2.v_save = a.siV, l2.mean = a.siM, l2.rstd = a.siR;
-    layernorm_fwd(l2, act, s);
+    lnf(l2, s);
   }
   static constexpr int kMfLayer = 62;  // dropout-site layer index of the decoder's move-first FFN
 
@@ -750,7 +784,7 @@ struct capgen_engine {
       g.key_ids = a.ids, g.kid_bs = Lq, g.pad_idx = cfg.pad_idx, g.causal = 1;
       g.temperature = std::sqrt((float)dkd);
       g.drop = mk_drop(pa, site(1, l, 3), drop_on);
-      attention_fwd(g, A.atts, keep_probs(g) ? A.Ps : nullptr, act, s);
+      attf(g, A.atts, keep_probs(g) ? A.Ps : nullptr, act, s);
       LnFwd l1;
       l1.M = Md, l1.d = dd, l1.a = a.tmp, l1.drop = mk_drop(p, site(1, l, 4), drop_on), l1.res = a.D[l];
       l1.gamma = P(w.lsg), l1.beta = P(w.lsb), l1.y = A.D1, l1.v_save = A.vs, l1.mean = A.ms, l1.rstd = A.rs;
@@ -766,7 +800,7 @@ struct capgen_engine {
       c.key_valid = a.valid, c.kv_bs = N;
       c.temperature = std::sqrt((float)dkd);
       c.drop = mk_drop(pa, site(1, l, 5), drop_on);
-      attention_fwd(c, A.attc, keep_probs(c) ? A.Pc : nullptr, act, s);
+      attf(c, A.attc, keep_probs(c) ? A.Pc : nullptr, act, s);
       LnFwd l2;
       l2.M = Md, l2.d = dd, l2.a = a.tmp, l2.drop = mk_drop(p, site(1, l, 6), drop_on), l2.res = A.D1;
       l2.gamma = P(w.lcg), l2.beta = P(w.lcb), l2.y = A.D2, l2.v_save = A.vc, l2.mean = A.mc, l2.rstd = A.rc;
@@ -870,6 +904,13 @@ struct capgen_engine {
     const char* e = std::getenv("CAPGEN_COLSUM_SIDE");
     return !(e && e[0] == '0');
   }();
+  // input-gradient partial products queued for es2 like the weight gradients (the encoder-output
+  // gradient per decoder block, split_enc_grad below); `mark`: record ev_part after this one
+  struct SideGemm {
+    GemmArgs ga;
+    bool mark;
+  };
+  std::vector<SideGemm> nn_pending;
   // es2 waits for everything issued on s so far, then runs the queued weight-gradient GEMMs
   void flush(hipStream_t s) {
     fork(s);
@@ -877,13 +918,38 @@ struct capgen_engine {
     dw_pending.clear();
     for (const ColJob& j : col_pending) column_sum(j.X, j.M, j.N, j.N, 1.f, nullptr, j.db, act, es2, NSTRIPE, n_small);
     col_pending.clear();
+    for (const SideGemm& j : nn_pending) {
+      gemm(j.ga, act, DType::F32, false, true, es2);
+      if (j.mark) CAPGEN_HIP(hipEventRecord(ev_part, es2));
+    }
+    nn_pending.clear();
+  }
+  // The gradient into the encoder output is sum_l gKV_l . Wkv_l over the decoder blocks' cross
+  // K/V (model.py:441-446 restated backward).  bf16 mode: block l's term (l >= 1) is accumulated
+  // into an f32 buffer on es2 as soon as block l's cross-attention backward has produced gKV_l
+  // (and its K/V weight gradient joins the block's grouped dW launch), so after the decoder only
+  // block 0's term is left on the critical stream -- one K = 2d GEMM whose epilogue adds the f32
+  // partial sum -- instead of one K = 2 d Ld GEMM.  Measured slower (3.45 vs 3.41 ms/step at
+  // C2: the side GEMMs queue behind the weight-gradient groups on es2 and the critical stream
+  // waits for them), so off unless CAPGEN_SPLIT_ENC_GRAD=1 (experiment knob)
+  bool split_enc_grad = [] {
+    const char* e = std::getenv("CAPGEN_SPLIT_ENC_GRAD");
+    return e && e[0] == '1';
+  }();
+  // GemmArgs of dX[M,K] (+)= dY[M,N] . W[N,K] (linear_dx) without launching it
+  GemmArgs dx_args(const void* dY, int64_t ldy, int64_t woff, int64_t ldw, void* dX, int64_t ldx, int M, int N,
+                   int K, int beta) const {
+    GemmArgs ga;
+    ga.M = M, ga.N = K, ga.K = N, ga.A = dY, ga.lda = ldy, ga.B = W(woff), ga.ldb = ldw, ga.C = dX, ga.ldc = ldx;
+    ga.beta = beta;
+    return ga;
   }
 
   // lb = the block's LayerNorm backward (dy = grad wrt block output, d_res -> r_out, d_a -> gA);
   // X = block input, H = hidden activations.
   void ffn_bwd(int M, int d, int f, const LnBwd& lb, const void* X, const void* H, int64_t W1, int64_t b1, int64_t W2,
                void* gH, hipStream_t s) {
-    layernorm_bwd(lb, act, s);
+    lnb(lb, s);
     void* gA = lb.d_a;
     dw_side(gA, d, H, f, W2, f, M, d, f, nullptr, s);
     const bool side = colsum_side && es2 != s;
@@ -902,7 +968,7 @@ struct capgen_engine {
       CAPGEN_HIP(hipMemcpyAsync(dbg_snap[3], lb.mean, (size_t)M * 4, hipMemcpyDeviceToDevice, s));
       CAPGEN_HIP(hipMemcpyAsync(dbg_snap[4], lb.rstd, (size_t)M * 4, hipMemcpyDeviceToDevice, s));
     }
-    layernorm_bwd(lb, act, s);
+    lnb(lb, s);
     if (snap) CAPGEN_HIP(hipMemcpyAsync(dbg_snap[1], lb.d_a, (size_t)M * d * es_(), hipMemcpyDeviceToDevice, s));
     dw_side(lb.d_a, d, att, d, Wo, d, M, d, d, nullptr, s);
     linear_dx(lb.d_a, d, Wo, d, gATT, d, M, d, d, 0, nullptr, nullptr, s);
@@ -981,7 +1047,7 @@ struct capgen_engine {
     if (valid) g.key_valid = valid, g.kv_bs = N, g.causal = 1;
     g.temperature = std::sqrt((float)dke);
     g.drop = mk_drop(pa, site(0, layer, 0), on);
-    attention_bwd(g, A.P, gb.gATT1, gb.gQKV, at(gb.gQKV, d), at(gb.gQKV, 2 * d), act, s);
+    attb(g, A.P, gb.gATT1, gb.gQKV, at(gb.gQKV, d), at(gb.gQKV, 2 * d), act, s);
     dw_side(gb.gQKV, 3 * d, X, d, w.Wqkv, d, Me, 3 * d, d, nullptr, s);
     linear_dx(gb.gQKV, 3 * d, w.Wqkv, d, gO, d, Me, 3 * d, d, 1, nullptr, nullptr, s);  // gO = grad wrt X
   }
@@ -990,15 +1056,13 @@ struct capgen_engine {
   void image_objects_bwd(const void* gX0, int B, int N, bool on, hipStream_t s) {
     const int Me = B * N, d = L.d;
     // second norm: grad wrt Z[2r+1] + Ep[r] (no residual, no dropout)
-    layernorm_bwd(lnb_desc(Me, d, gX0, a.siV, a.siM, a.siR, L.enc_lng, L.enc_lnb, -1, RowMask{}, Drop{}, nullptr,
-                           a.siGEp),
-                  act, s);
+    lnb(lnb_desc(Me, d, gX0, a.siV, a.siM, a.siR, L.enc_lng, L.enc_lnb, -1, RowMask{}, Drop{}, nullptr,
+                           a.siGEp), s);
     pair_scatter(a.siGEp, Me, d, a.siG0, act, s);  // only the region token's output is kept
     enc_layer_bwd(L.img, a.si, a.gsi, a.siX2, Me, 2, a.siValid, kImgLayer, on, a.siG0, a.siG1, s);
     pair_reduce(a.siG0, B, N, d, a.siGY, act, s);  // image-row tokens fold back onto region 0
-    layernorm_bwd(lnb_desc(Me, d, a.siGY, a.ev0, a.em0, a.er0, L.enc_lng, L.enc_lnb, -1, RowMask{}, Drop{}, nullptr,
-                           a.gAe),
-                  act, s);
+    lnb(lnb_desc(Me, d, a.siGY, a.ev0, a.em0, a.er0, L.enc_lng, L.enc_lnb, -1, RowMask{}, Drop{}, nullptr,
+                           a.gAe), s);
     // feature columns see the first embedding only; position columns both (+ Ep after the block)
     linear_dw(a.gAe, d, a.Aenc, L.Kp, L.enc_emb_W, L.Kp, Me, d, L.F, nullptr, s);
     add_inplace(a.siGEp, a.gAe, (int64_t)Me * d, act, s);
@@ -1011,7 +1075,7 @@ struct capgen_engine {
     const int dd = L.dd, fd = L.fd;
     const LnBwd lb = lnb_desc(Md, dd, a.gOut, a.mfV, a.mfM, a.mfR, L.mf_lng, L.mf_lnb, L.mf_b2, RowMask{},
                               mk_drop(cfg.dropout, site(1, kMfLayer, 0), on), a.gRes, a.mfGA);
-    layernorm_bwd(lb, act, s);
+    lnb(lb, s);
     dw_side(a.mfGA, dd, a.mfH, fd, L.mf_W2, fd, Md, dd, fd, nullptr, s);
     linear_dx(a.mfGA, dd, L.mf_W2, fd, a.mfGH, fd, Md, dd, fd, 0, a.mfH, nullptr, s, GS(L.mf_b1));
     dw_side(a.mfGH, fd, a.mfU, dd, L.mf_W1, dd, Md, fd, dd, nullptr, s);
@@ -1068,6 +1132,7 @@ struct capgen_engine {
     bucket(L.Wc, L.n_dense - L.Wc, s);  // flushed after the dX GEMM above: it reads Wc
 
     const int64_t kvld = (int64_t)L.Ld * 2 * dd;
+    const bool split_kv = split_enc_grad && act == DType::BF16 && es2 != s && L.Ld > 1;
     void* gO = a.gOut;
     void* gR = a.gRes;
     if (L.has_mf) {  // gRes = grad wrt D[Ld]; a.mfGU = grad wrt U (its encoder part is added below)
@@ -1090,8 +1155,15 @@ struct capgen_engine {
       c.key_valid = a.valid, c.kv_bs = N;  // masks as in forward (the MFMA backward recomputes P)
       c.temperature = std::sqrt((float)dkd);
       c.drop = mk_drop(pa, site(1, l, 5), on);
-      attention_bwd(c, A.Pc, gb.gATT2, gb.gQc, at(a.gKV, (int64_t)l * 2 * dd), at(a.gKV, (int64_t)l * 2 * dd + dd),
-                    act, s);
+      attb(c, A.Pc, gb.gATT2, gb.gQc, at(a.gKV, (int64_t)l * 2 * dd), at(a.gKV, (int64_t)l * 2 * dd + dd), act, s);
+      if (split_kv) {  // this block's cross K/V: weight gradient and (l >= 1) encoder-output term
+        dw_side(at(a.gKV, (int64_t)l * 2 * dd), kvld, a.X[L.Le], d, L.Wkv_all + (int64_t)l * 2 * dd * d, d, Me,
+                2 * dd, d, nullptr, s);
+        if (l >= 1)
+          nn_pending.push_back(SideGemm{dx_args(at(a.gKV, (int64_t)l * 2 * dd), kvld, L.Wkv_all + (int64_t)l * 2 * dd * d,
+                                                d, a.gEnc32, d, Me, 2 * dd, d, l != L.Ld - 1),
+                                        l == 1});
+      }
       dw_side(gb.gQc, dd, A.D1, dd, w.Wq_c, dd, Md, dd, dd, nullptr, s);
       linear_dx(gb.gQc, dd, w.Wq_c, dd, gO, dd, Md, dd, dd, 1, nullptr, nullptr, s);  // gO = grad wrt D1
       mha_out_bwd(Md, dd, lself, A.atts, w.Wo_s, gb.gATT1, s);  // gR = grad wrt D_l (residual part)
@@ -1104,7 +1176,7 @@ struct capgen_engine {
       g.key_ids = a.ids, g.kid_bs = Lq, g.pad_idx = cfg.pad_idx, g.causal = 1;  // as in forward
       g.temperature = std::sqrt((float)dkd);
       g.drop = mk_drop(pa, site(1, l, 3), on);
-      attention_bwd(g, A.Ps, gb.gATT1, gb.gQKV, at(gb.gQKV, dd), at(gb.gQKV, 2 * dd), act, s);
+      attb(g, A.Ps, gb.gATT1, gb.gQKV, at(gb.gQKV, dd), at(gb.gQKV, 2 * dd), act, s);
       dw_side(gb.gQKV, 3 * dd, a.D[l], dd, w.Wqkv, dd, Md, 3 * dd, dd, nullptr, s);
       linear_dx(gb.gQKV, 3 * dd, w.Wqkv, dd, gR, dd, Md, 3 * dd, dd, 1, nullptr, nullptr, s);
       if (l % bucket_blocks == 0)  // blocks l .. l + bucket_blocks - 1 (contiguous in the arena)
@@ -1118,7 +1190,7 @@ struct capgen_engine {
     {
       const LnBwd lb = dec_emb_lb(gO);
       flush(s);
-      layernorm_bwd(lb, act, es2);
+      lnb(lb, es2);
       linear_dx(a.gAd, dd, L.Wel, L.dwe, a.gE, L.dwe, Md, dd, L.dwe, 0, nullptr, nullptr, es2);
       const DwJob wel{a.gAd, a.E, dd, L.dwe, L.Wel, L.dwe, Md, dd, L.dwe, nullptr};
       dw_launch(&wel, 1, es2);
@@ -1130,10 +1202,17 @@ struct capgen_engine {
     // it runs on the other residual buffer and on tmp (free during backward)
     gO = eO;
     gR = a.tmp;
-    linear_dx(a.gKV, kvld, L.Wkv_all, d, gO, d, Me, L.Ld * 2 * dd, d, 0, nullptr, nullptr, s);
+    if (split_kv) {  // block 0's term + the f32 sum of blocks Ld-1 .. 1 (summed on es2)
+      CAPGEN_HIP(hipStreamWaitEvent(s, ev_part, 0));
+      GemmArgs ga = dx_args(a.gKV, kvld, L.Wkv_all, d, gO, d, Me, 2 * dd, d, 0);
+      ga.cin = a.gEnc32, ga.ldcin = d, ga.prio = prio(s);
+      gemm(ga, act, act, false, true, s);
+    } else {
+      linear_dx(a.gKV, kvld, L.Wkv_all, d, gO, d, Me, L.Ld * 2 * dd, d, 0, nullptr, nullptr, s);
+    }
     if (dbg_stop == 1) return join(s);  // diagnostic (CAPGEN_DEBUG_BWD_STOP): capgen_debug_copy_buffer
     if (L.has_mf) first_region_grad(a.mfGU, B, Lq, N, d, gO, act, s);  // enc[:, 0] of U = D + enc[:, 0]
-    dw_side(a.gKV, kvld, a.X[L.Le], d, L.Wkv_all, d, Me, L.Ld * 2 * dd, d, nullptr, s);
+    if (!split_kv) dw_side(a.gKV, kvld, a.X[L.Le], d, L.Wkv_all, d, Me, L.Ld * 2 * dd, d, nullptr, s);
     // the decoder-embedding branch (es2) has been issued: every decoder-side gradient is final
     // the flush of the first bucket follows the dX GEMM above (it reads Wkv_all); es2 then holds
     // every producer of the other three buckets
@@ -1155,7 +1234,7 @@ struct capgen_engine {
       image_objects_bwd(gO, B, N, on, s);
       flush(s);  // the image block's weight gradients share the embedding bucket
     } else {
-      layernorm_bwd(enc_emb_lb(gO), act, s);
+      lnb(enc_emb_lb(gO), s);
       linear_dw(a.gAe, d, a.Aenc, L.Kp, L.enc_emb_W, L.Kp, Me, d, L.Kp, nullptr, s);
     }
     // every encoder LayerNorm/bias partial was accumulated on s; in step mode the fold and the
@@ -1355,7 +1434,7 @@ struct capgen_engine {
       linear(a.Aenc, L.Kp, L.enc_emb_W, L.Kp, a.tmp, d, act, Me, d, L.Kp, nullptr, 0, s);
       LnFwd ln;
       ln.M = Me, ln.d = d, ln.a = a.tmp, ln.gamma = P(L.enc_lng), ln.beta = P(L.enc_lnb), ln.y = a.X[0];
-      layernorm_fwd(ln, act, s);
+      lnf(ln, s);
     }
     RowMask emask{};
     if (cfg.encode_mask) emask.valid = a.valid;
@@ -1371,17 +1450,17 @@ struct capgen_engine {
       g.o_ld = d, g.o_bs = (int64_t)N * d;
       if (cfg.encode_mask) g.key_valid = a.valid, g.kv_bs = N, g.causal = 1;
       g.temperature = std::sqrt((float)dke);
-      attention_fwd(g, A.att, nullptr, act, s);
+      attf(g, A.att, nullptr, act, s);
       linear(A.att, d, w.Wo, d, a.tmp, d, act, Me, d, d, nullptr, 0, s);
       LnFwd l1;
       l1.M = Me, l1.d = d, l1.a = a.tmp, l1.res = a.X[l], l1.gamma = P(w.ln1g), l1.beta = P(w.ln1b), l1.y = A.Y;
-      layernorm_fwd(l1, act, s);
+      lnf(l1, s);
       linear(A.Y, d, w.W1, d, A.H, L.fe, act, Me, L.fe, d, P(w.b1), 1, s);
       linear(A.H, L.fe, w.W2, L.fe, a.tmp, d, act, Me, d, L.fe, nullptr, 0, s);
       LnFwd l2;
       l2.M = Me, l2.d = d, l2.a = a.tmp, l2.a_bias = P(w.b2), l2.res = A.Y, l2.gamma = P(w.ln2g);
       l2.beta = P(w.ln2b), l2.mask = emask, l2.y = a.X[l + 1];
-      layernorm_fwd(l2, act, s);
+      lnf(l2, s);
     }
     linear(a.X[L.Le], d, L.Wkv_all, d, a.KV, (int64_t)L.Ld * 2 * L.dd, act, Me, L.Ld * 2 * L.dd, d, nullptr, 0, s);
   }
@@ -1442,7 +1521,7 @@ struct capgen_engine {
     LnFwd ln;
     ln.M = R, ln.d = dd, ln.a = g.tmp, ln.pe = pe + (int64_t)t * dd, ln.pe_L = 1, ln.gamma = P(L.dec_lng);
     ln.beta = P(L.dec_lnb), ln.y = g.x;
-    layernorm_fwd(ln, act, s);
+    lnf(ln, s);
     RowMask rm{};
     rm.ids = ids + t, rm.ids_ld = Tc, rm.pad_idx = cfg.pad_idx;
     const int64_t kvld = (int64_t)L.Ld * 2 * dd, cld = (int64_t)Tc * 2 * dd;
@@ -1460,11 +1539,11 @@ struct capgen_engine {
       sg.o_ld = dd, sg.o_bs = dd;
       sg.key_ids = ids, sg.kid_bs = Tc, sg.pad_idx = cfg.pad_idx, sg.causal = 1, sg.q_pos0 = t;
       sg.temperature = std::sqrt((float)dkd);
-      attention_fwd(sg, g.att, nullptr, act, s);
+      attf(sg, g.att, nullptr, act, s);
       linear(g.att, dd, w.Wo_s, dd, g.tmp, dd, act, R, dd, dd, nullptr, 0, s);
       LnFwd l1;
       l1.M = R, l1.d = dd, l1.a = g.tmp, l1.res = g.x, l1.gamma = P(w.lsg), l1.beta = P(w.lsb), l1.y = g.x1;
-      layernorm_fwd(l1, act, s);
+      lnf(l1, s);
       linear(g.x1, dd, w.Wq_c, dd, g.q, dd, act, R, dd, dd, nullptr, 0, s);
       AttnGeom c;
       c.B = R, c.H = Hd, c.Lq = 1, c.Lk = N, c.dk = dkd;
@@ -1475,17 +1554,17 @@ struct capgen_engine {
       c.o_ld = dd, c.o_bs = dd;
       c.key_valid = a.valid, c.kv_bs = N;
       c.temperature = std::sqrt((float)dkd);
-      attention_fwd(c, g.att, (want_attn && l == L.Ld - 1) ? g.Pc : nullptr, act, s);
+      attf(c, g.att, (want_attn && l == L.Ld - 1) ? g.Pc : nullptr, act, s);
       linear(g.att, dd, w.Wo_c, dd, g.tmp, dd, act, R, dd, dd, nullptr, 0, s);
       LnFwd l2;
       l2.M = R, l2.d = dd, l2.a = g.tmp, l2.res = g.x1, l2.gamma = P(w.lcg), l2.beta = P(w.lcb), l2.y = g.x2;
-      layernorm_fwd(l2, act, s);
+      lnf(l2, s);
       linear(g.x2, dd, w.W1, dd, g.h, L.fd, act, R, L.fd, dd, P(w.b1), 1, s);
       linear(g.h, L.fd, w.W2, L.fd, g.tmp, dd, act, R, dd, L.fd, nullptr, 0, s);
       LnFwd l3;
       l3.M = R, l3.d = dd, l3.a = g.tmp, l3.a_bias = P(w.b2), l3.res = g.x2, l3.gamma = P(w.lfg), l3.beta = P(w.lfb);
       l3.mask = rm, l3.y = g.x;
-      layernorm_fwd(l3, act, s);
+      lnf(l3, s);
     }
     const void* xo = g.x;
     if (L.has_mf) {  // rows r -> image r % Bimg
@@ -1583,7 +1662,7 @@ struct capgen_engine {
     if (ev_out) (void)hipEventDestroy(ev_out);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
-    for (hipEvent_t e : {ev_b1, ev_b2, ev_cj, ev_count})
+    for (hipEvent_t e : {ev_b1, ev_b2, ev_cj, ev_count, ev_part})
       if (e) (void)hipEventDestroy(e);
     if (ec && ec != es && ec != es2) (void)hipStreamSynchronize(ec), (void)hipStreamDestroy(ec);
     if (es2 && es2 != es) (void)hipStreamSynchronize(es2), (void)hipStreamDestroy(es2);
@@ -1682,7 +1761,7 @@ int capgen_create(const capgen_config* cfg, int device, capgen_t** out) {
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
     if (nstreams >= 3) CAPGEN_HIP(hipStreamCreateWithFlags(&h->ec, hipStreamNonBlocking));
     else h->ec = h->es2;
-    for (hipEvent_t* e : {&h->ev_b1, &h->ev_b2, &h->ev_cj})
+    for (hipEvent_t* e : {&h->ev_b1, &h->ev_b2, &h->ev_cj, &h->ev_part})
       CAPGEN_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_count, hipEventDisableTiming));

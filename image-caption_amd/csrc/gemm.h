@@ -22,6 +22,9 @@ struct GemmArgs {
   float alpha = 1.f;
   const float* alpha_ptr = nullptr;  // device scalar multiplied into alpha (e.g. 1/count)
   int beta = 0;                      // 1: accumulate into C
+  int prio = 0;                      // 1: critical-path launch, waves raise their issue priority
+  const float* cin = nullptr;        // += cin[m][n] (f32, row stride ldcin) before the activation
+  int64_t ldcin = 0;
   int relu = 0;
   float* colsum = nullptr;           // += column sums of the (post-epilogue, beta=0) output, f32 [N]
   int colsum_stripes = 1;            // workgroup w adds into colsum + (w % stripes) * colsum_stride

@@ -221,6 +221,7 @@ void gemm(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t 
   require(((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0, "gemm: operands must be 16-B aligned");
   require(g.K > 0, "gemm: K must be positive");
   require(!g.colsum || !g.beta, "gemm: colsum requires beta == 0");
+  require(!g.cin || in == DType::BF16, "gemm: cin is a bf16-path epilogue input");
   if (in == DType::F32) {
     if (out == DType::F32) launch_layout<float, float>(g, ta, tb, s);
     else launch_layout<float, bf16>(g, ta, tb, s);

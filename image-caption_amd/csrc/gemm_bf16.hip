@@ -75,12 +75,16 @@ struct Op {
   // The operand is read through a buffer resource (bounds-checked: an offset past num_records
   // returns zeros), so the k-loop issues each 1-KB piece with NO per-piece address arithmetic:
   // every lane's byte offset is fixed for the tile (voff, set up once) and the k-tile advance is
-  // one scalar soffset (kstep per tile).  Rows past the tile's extent read past num_records
-  // (non-TRANS: rows >= R; TRANS: k rows >= K); a chunk past the minor extent (TRANS: columns
-  // >= R) gets the OOB offset once; only a non-TRANS K tail needs a per-tile lane mask.
+  // one scalar soffset (kstep per tile).  Nothing is left to num_records: a chunk outside the
+  // tile's extent (non-TRANS: rows >= R; TRANS: columns >= R) gets the OOB offset once, and the
+  // K tail (non-TRANS: k columns >= K; TRANS: k rows >= K) is masked per lane on the last
+  // k-tile.  (The first version left the TRANS k rows >= K of a tile with soff > 0 to the range
+  // check: the bf16 step's encoder weight gradients -- K = 72 tokens, two k-tiles -- then
+  // differed between identical runs in 9 of 16 probes, 0 of 16 with the mask,
+  // tools/step_det_probe.py; a standalone GEMM over NaN-poisoned neighbours did not show it.)
   __amdgpu_buffer_rsrc_t rsrc;
   uint32_t voff[PER_WAVE];
-  int kch[PER_WAVE];  // non-TRANS: k offset of the lane's chunk inside the tile
+  int kch[PER_WAVE];  // k offset of the lane's chunk (non-TRANS: column, TRANS: row) in the tile
   uint32_t kstep;
 
   __device__ __forceinline__ void setup(const bf16* src, int64_t ld, int r0, int R, int K, int kt_first, int wave,
@@ -98,7 +102,7 @@ struct Op {
         voff[j] = r0 + row < R ? (uint32_t)(((int64_t)(r0 + row) * ld + (int64_t)kt_first * BK + ch * 8) * 2) : OOB;
       } else {
         const int k = b / (ROWS * 2), ch = swz_t<ROWS>(k, (b % (ROWS * 2)) >> 4);
-        kch[j] = 0;
+        kch[j] = k;
         voff[j] = r0 + ch * 8 < R ? (uint32_t)((((int64_t)kt_first * BK + k) * ld + r0 + ch * 8) * 2) : OOB;
       }
     }
@@ -108,7 +112,7 @@ struct Op {
   // img; tail: the tile ends past K (kb = its first k)
   __device__ __forceinline__ void issue(int t, char* img, bool tail, int kb, int K, int wave) const {
     const uint32_t soff = (uint32_t)t * kstep;
-    if (!TRANS && tail) {  // uniform: the last k-tile of a K that is not a multiple of 64
+    if (tail) {  // uniform: the last k-tile of a K that is not a multiple of 64
 #pragma unroll
       for (int j = 0; j < PER_WAVE; ++j) dma(kb + kch[j] < K ? voff[j] : OOB, soff, img + (wave + NW * j) * 1024);
     } else {
@@ -397,6 +401,12 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&a
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = alpha * acc[i][j][r] + bn[r];
+      if (g.cin) {
+        float c4[4];
+        load4<float>(g.cin + (int64_t)m * g.ldcin + n, c4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += c4[r];
+      }
       if (aux) {
         float a4[4];
         load4<bf16>(aux + (int64_t)m * g.ldaux + n, a4);
@@ -446,6 +456,9 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmArgs g, int
                                                                 const void* zero, int splitk, float* ws,
                                                                 int* tile_cnt, int group_m, int proto) {
   __shared__ __attribute__((aligned(1024))) char smem[TileCfg<TA, TB, BM, BN, WM, WN, STAGES>::SMEM];
+  // critical-path launch (GemmArgs::prio): beside the side streams' weight-gradient / Adam waves
+  // on the same CUs, the SIMD arbiter issues this kernel's instructions first
+  if (g.prio) __builtin_amdgcn_s_setprio(3);
   const int slot = xcd_slot(blockIdx.x, nblk);
   const int tile = slot / splitk, split = slot % splitk;  // split-K slices of a tile are adjacent
   // tiles in column-major groups of group_m tile rows: an XCD's contiguous slot range covers a

@@ -8,6 +8,7 @@ namespace capgen {
 // y = LN(drop(a + a_bias) + res + pe[m % pe_L]) * rowmask          (modules.py:86-90, 114-120)
 struct LnFwd {
   int M = 0, d = 0;
+  int prio = 0;  // 1: the critical-path kernel raises its waves' issue priority (s_setprio)
   const void* a = nullptr;
   const float* a_bias = nullptr;
   Drop drop{};
@@ -26,6 +27,7 @@ void layernorm_fwd(const LnFwd& a, DType t, hipStream_t s);
 
 struct LnBwd {
   int M = 0, d = 0;
+  int prio = 0;  // as LnFwd::prio
   const void* dy = nullptr;
   const void* v = nullptr;
   const float* mean = nullptr;

@@ -33,6 +33,7 @@ __device__ __forceinline__ void load_f32(const float* p, float (&out)[DPL]) {
 }
 template <typename T, int DPL>
 __global__ void __launch_bounds__(LN_THREADS) ln_fwd_kernel(LnFwd a) {
+  if (a.prio) __builtin_amdgcn_s_setprio(3);
   const int lane = threadIdx.x & 63;
   const int m = blockIdx.x * (LN_THREADS / 64) + (threadIdx.x >> 6);
   if (m >= a.M) return;
@@ -91,6 +92,7 @@ __global__ void __launch_bounds__(LN_THREADS) ln_fwd_kernel(LnFwd a) {
 template <typename T, int DPL>
 __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(LnBwd a) {
   __shared__ float red[3][LN_THREADS / 64][64 * DPL];
+  if (a.prio) __builtin_amdgcn_s_setprio(3);
   constexpr int R = 2;  // rows in flight per wave: every load of both rows is issued first
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int d = a.d, c0 = lane * DPL;

@@ -373,6 +373,29 @@ def test_train_step_equals_forward_backward_adam_bf16(graph):
         assert abs(la.item() - lb.item()) < 1e-3 * abs(lb.item())
 
 
+def test_bf16_weight_gradients_bit_reproducible():
+    """Two engines with the same weights and batch produce bit-identical Linear weight gradients
+    in bf16 mode, four times over (every GEMM, the split-K combine and the grouped launches are
+    deterministic; only LayerNorm/bias sums use f32 atomics).  c2s has 2 x 36 = 72 encoder
+    tokens: the weight-gradient GEMMs' K runs 8 rows into a second k-tile, the case whose tail
+    once read past the activation (gemm_bf16.hip Op::issue; 9 of 16 runs diverged)."""
+    cfg, seed, z = load_fixture("c2s")
+    f, p, c = _inputs(z)
+    for _ in range(4):
+        grads = []
+        for _e in range(2):
+            e = _engine(cfg, seed, dtype="bf16")
+            e.set_training(False)
+            e.forward(f, p, c)
+            e.backward()
+            grads.append(e.grads_state_dict())
+            torch.cuda.synchronize()
+        ga, gb = grads
+        bad = [k for k in ga if ga[k].dim() == 2 and k != "decoder.word_embedding.weight"
+               and not torch.equal(ga[k], gb[k])]
+        assert not bad, bad
+
+
 def test_dropout_backward_directional_derivative_fp32():
     """Train-mode (dropout on) gradient vs a central finite difference of the same
     dropout mask (RNG reset before each forward)."""
@@ -458,6 +481,44 @@ def test_gemm_every_variant_and_splitk(variant, ta, tb):
             assert (Cd.cpu() - ref).abs().max().item() <= 2e-3 * np.sqrt(K)
     finally:
         _lib.check(lib.capgen_debug_gemm_variant(0))
+
+
+@pytest.mark.parametrize("variant", [0, 6, 17, 303, 813])
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("K", [72, 1000])
+def test_gemm_k_tail_never_reads_past_the_operands(variant, ta, tb, K):
+    """Both operands sit in buffers whose bytes past the matrix (and past each row's K) are NaN:
+    the k-loop's bounds handling must zero the K tail of the last k-tile whatever follows the
+    operand -- a weight gradient over B*N = 72 tokens (two k-tiles, the second 8 deep) once read
+    rows 72..127 of the activation's neighbour (nondeterministic encoder gradients)."""
+    import ctypes as C
+    from capgen import _lib
+    lib = _lib.load()
+    M, N = 136, 200
+    g = torch.Generator(device="cpu").manual_seed(K + 10 * ta + 20 * tb + variant)
+    A = torch.randn(M, K, generator=g).bfloat16()
+    Bm = torch.randn(N, K, generator=g).bfloat16()
+    ref = A.float() @ Bm.float().t()
+
+    def poisoned(x):  # x in a NaN-filled buffer with 128 spare rows and 64 spare columns
+        buf = torch.full((x.shape[0] + 128, x.shape[1] + 64), float("nan"), dtype=torch.bfloat16, device=DEV)
+        buf[: x.shape[0], : x.shape[1]] = x.to(DEV)
+        return buf
+
+    Ad = poisoned(A.t().contiguous() if ta else A)
+    Bd = poisoned(Bm.t().contiguous() if tb else Bm)
+    Cd = torch.full((M, N), float("nan"), dtype=torch.float32, device=DEV)
+    _lib.check(lib.capgen_debug_gemm_variant(variant))
+    try:
+        _lib.check(lib.capgen_debug_gemm(M, N, K, C.c_void_p(Ad.data_ptr()), Ad.shape[1], ta,
+                                         C.c_void_p(Bd.data_ptr()), Bd.shape[1], tb, C.c_void_p(Cd.data_ptr()),
+                                         N, 1, 0, None, 1.0, 0, 0, None))
+        torch.cuda.synchronize()
+    finally:
+        _lib.check(lib.capgen_debug_gemm_variant(0))
+    out = Cd.cpu()
+    assert torch.isfinite(out).all(), int((~torch.isfinite(out)).sum())
+    assert (out - ref).abs().max().item() <= 2e-3 * np.sqrt(K)
 
 
 def test_splitk_combine_bit_reproducible_under_load():

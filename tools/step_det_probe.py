@@ -33,6 +33,8 @@ if os.environ.get("PROBE_PROTO"):  # split-K hand-off protocol bits (capgen_debu
 n_diff = 0
 for it in range(int(sys.argv[1]) if len(sys.argv) > 1 else 6):
     a, b, c2 = mk(), mk(), mk()
+    if os.environ.get("PROBE_GRAPH") == "1":
+        a.set_graph(True)          # the whole step as one captured graph
     a.train_step(f, p, c)          # bucketed step
     if os.environ.get("PROBE_SYNC") == "1":
         torch.cuda.synchronize()   # no overlap between the engines
@@ -42,6 +44,8 @@ for it in range(int(sys.argv[1]) if len(sys.argv) > 1 else 6):
         e.backward()
         grads.append(e.grads_state_dict())
         e.adam_step()
+        if os.environ.get("PROBE_SYNC") == "1":
+            torch.cuda.synchronize()
     gb, gc = grads
     worst = max(((gb[k].double() - gc[k].double()).norm() / (gb[k].double().norm() + 1e-30)).item() for k in gb
                 if k.startswith("encoder.") or k.startswith("decoder.decoder."))
