@@ -13,7 +13,12 @@ import torch
 
 from .config import CapgenConfig
 from .model import PolicyNetwork, Transformer
+from .staging import HostBatchStager
 from .utils import decode_captions, load_word_to_idx
+
+
+def _on_device(t) -> bool:
+    return isinstance(t, torch.Tensor) and t.is_cuda
 
 
 class MODEL_init:
@@ -66,6 +71,7 @@ class TRANSFORMER(MODEL_init):
         self.device = torch.device(device)
         self.model = Transformer.from_config(cfg, self.device, state_dict=state_dict)
         self._stage = {}
+        self._host_stager = None
 
     def _staged(self, name, t, dtype):
         buf = self._stage.get(name)
@@ -76,7 +82,19 @@ class TRANSFORMER(MODEL_init):
         return buf
 
     def train_step(self, batch_features, batch_positions, batch_captions):
-        """models.py:115-126: zero_grad + forward + backward + Adam, one engine call."""
+        """models.py:115-126: zero_grad + forward + backward + Adam, one engine call.
+
+        Host (CPU / numpy) batches -- what main.py's DataLoader yields -- go through pinned,
+        double-buffered staging with the copy on a side stream, overlapped with the previous
+        step (capgen.staging.HostBatchStager); device tensors are staged by a D2D copy."""
+        if not _on_device(batch_features):
+            st = self._host_stager
+            if st is None or not st.fits(batch_features, batch_positions, batch_captions):
+                B, N, F = batch_features.shape
+                st = self._host_stager = HostBatchStager(self.device, B, N, F, batch_positions.shape[2],
+                                                         batch_captions.shape[1])
+            st.run(self.model.engine, batch_features, batch_positions, batch_captions)
+            return
         fdt = torch.bfloat16 if self.config.dtype == "bf16" else torch.float32
         f = self._staged("f", batch_features, fdt)
         p = self._staged("p", batch_positions, torch.float32)

@@ -723,6 +723,40 @@ def test_resident_store_indexed_train_step_equals_copied_batch():
     assert torch.isfinite(loss).all() or torch.isnan(loss).all()  # all-padding images may be NaN, as in the reference
 
 
+def test_transformer_host_batches_equal_device_batches():
+    """TRANSFORMER.train_step with CPU batches (pinned double-buffered staging, side-stream H2D,
+    indexed step: capgen/staging.py) == the same steps with device batches: five batches that
+    reuse both staging slots, then a smaller last batch (new staging buffers)."""
+    from capgen.models import TRANSFORMER
+    from capgen.synthetic import synthetic_batch
+    cfg, seed, z = load_fixture("c1")
+    w2i = {"<NULL>": 0, "<START>": 1, "<END>": 2}
+    w2i.update({f"w{i}": i for i in range(3, cfg.num_vocab)})
+    sd = fixture_state_dict(cfg, seed=seed, with_buffer=False)
+    host = TRANSFORMER(cfg, word_to_idx=w2i, device=DEV, state_dict=sd)
+    dev = TRANSFORMER(cfg, word_to_idx=w2i, device=DEV, state_dict=sd)
+    for m in (host, dev):
+        m.model.engine.set_training(False)
+    batches = [synthetic_batch(6, 9, cfg.encode_dim_features, cfg.encode_dim_positions, 7, cfg.num_vocab,
+                               seed=40 + i, min_valid=2) for i in range(5)]
+    batches.append(synthetic_batch(3, 9, cfg.encode_dim_features, cfg.encode_dim_positions, 7, cfg.num_vocab,
+                                   seed=50, min_valid=2))
+    for i, (f, p, c) in enumerate(batches):
+        host.train_step(f, p, c)  # CPU tensors
+        dev.train_step(f.to(DEV), p.to(DEV), c.to(DEV))
+        lh = host.model.engine._loss.clone()
+        ld = dev.model.engine._loss.clone()
+        torch.cuda.synchronize()
+        if i == 0:
+            assert lh.item() == ld.item()
+        else:  # later steps: f32-atomic LN/bias gradient sums may differ in the last bits
+            assert abs(lh.item() - ld.item()) < 1e-5 * abs(ld.item())
+    assert host._host_stager.shape[0] == 3
+    sh, sv = host.model.engine.state_dict(False), dev.model.engine.state_dict(False)
+    for k in sh:
+        torch.testing.assert_close(sh[k], sv[k], atol=1e-5, rtol=0)
+
+
 def _edge_batch(case, F, Pd, V):
     """Edge-case inputs (SURVEY §8(a) A2/A10/A12 masks): minimum and maximum shapes, ragged
     N/T, a caption that is padding after START, an image with one valid region, an image whose

@@ -4,7 +4,8 @@
 # writes gpurun_out/<tag>/: bench.json (the bench line, CPU baseline included), the rocprofv3
 # kernel-trace + stats of a profiled bench run (kernel_stats.csv, timeline.txt with the
 # dominant-GEMM launches' trace average), and the HBM traffic of one step from two separate PMC
-# passes (pmc_traffic.json; FETCH_SIZE x2 per the gfx950 correction, WRITE_SIZE as is).
+# passes (pmc_traffic.json; FETCH_SIZE x2 per the gfx950 correction, WRITE_SIZE as is), and the
+# MFMA utilisation per kernel class from a third PMC pass (pmc_mfma.json, tools/pmc_mfma.py).
 set -o pipefail
 export TMPDIR=/tmp
 tag=${1:-r01}
@@ -24,3 +25,7 @@ for c in FETCH_SIZE WRITE_SIZE; do
     python3 bench.py --steps 6 --warmup 3 --no-cpu-baseline > "$out/pmc_$c.log" 2>&1 || { tail -20 "$out/pmc_$c.log"; exit 1; }
 done
 python tools/pmcsum.py "$out/pmc_FETCH_SIZE" "$out/pmc_WRITE_SIZE" "$out/pmc_traffic.json" | head -4
+timeout -s KILL 90 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv \
+  -d "$out/pmc_mfma" -o run -- python3 bench.py --steps 6 --warmup 3 --no-cpu-baseline > "$out/pmc_mfma.log" 2>&1 \
+  || { tail -20 "$out/pmc_mfma.log"; exit 1; }
+python tools/pmc_mfma.py "$out/pmc_mfma" "$out/pmc_mfma.json" | head -6
