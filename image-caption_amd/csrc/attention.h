@@ -13,6 +13,9 @@ struct AttnGeom {
   const void* k = nullptr; int64_t k_ld = 0, k_bs = 0;
   const void* v = nullptr; int64_t v_ld = 0, v_bs = 0;
   int kv_bmod = 0;                    // > 0: K/V/key_valid of query batch b come from batch b % kv_bmod
+  // decode only (Lq = 1): key j of query batch b is stored in batch kv_row[b*kv_row_ld + j]
+  // (beam search: a beam's cached K/V positions live in the rows of the beams it descends from)
+  const int32_t* kv_row = nullptr; int64_t kv_row_ld = 0;
   int64_t o_ld = 0, o_bs = 0;         // layout of O (forward output) and dO (backward input)
   // key mask: key (b, j) is masked if key_valid[b*kv_bs + j] == 0, or key_ids[b*kid_bs + j] == pad
   const uint8_t* key_valid = nullptr; int64_t kv_bs = 0;

@@ -51,13 +51,16 @@ __device__ __forceinline__ void st4(T* p, float4 v, float mul) {
 // rows x dk tile -> LDS [rows_padded][ldd] f32 (x / div), zero pad row when rows is odd
 template <typename T>
 __device__ __forceinline__ void stage_rows(float* dst, int ldd, const T* src, int64_t ld, int rows, int dk,
-                                           float div, int tid) {
+                                           float div, int tid, const int32_t* rowmap = nullptr, int64_t row_bs = 0,
+                                           int base_row = 0) {
   constexpr int V = 16 / sizeof(T);
   const int cpr = dk / V;
   for (int c = tid; c < rows * cpr; c += AT_THREADS) {
     const int r = c / cpr, d = (c % cpr) * V;
     float x[V];
-    load_f<T, V>(src + (int64_t)r * ld + d, x);
+    // rowmap (AttnGeom::kv_row): row r of this batch is stored in batch rowmap[r]
+    const int64_t roff = rowmap ? (int64_t)(rowmap[r] - base_row) * row_bs : 0;
+    load_f<T, V>(src + roff + (int64_t)r * ld + d, x);
 #pragma unroll
     for (int e = 0; e < V; ++e) dst[r * ldd + d + e] = div == 1.f ? x[e] : x[e] / div;
   }
@@ -109,8 +112,9 @@ __global__ void __launch_bounds__(AT_THREADS) attn_fwd_kernel(AttnGeom g, T* __r
   const T* k = reinterpret_cast<const T*>(g.k) + (int64_t)bk * g.k_bs + h * dk;
   const T* v = reinterpret_cast<const T*>(g.v) + (int64_t)bk * g.v_bs + h * dk;
   stage_rows<T>(Qs, ldd, q, g.q_ld, Lq, dk, g.temperature, tid);
-  stage_rows<T>(Ks, ldd, k, g.k_ld, Lk, dk, 1.f, tid);
-  stage_rows<T>(Vs, ldd, v, g.v_ld, Lk, dk, 1.f, tid);
+  const int32_t* rowmap = g.kv_row ? g.kv_row + (int64_t)b * g.kv_row_ld : nullptr;
+  stage_rows<T>(Ks, ldd, k, g.k_ld, Lk, dk, 1.f, tid, rowmap, g.k_bs, bk);
+  stage_rows<T>(Vs, ldd, v, g.v_ld, Lk, dk, 1.f, tid, rowmap, g.v_bs, bk);
   __syncthreads();
 
   gram(Qs, Ks, ldd, Lq, Lk, dk, S, lds_s, tid);
@@ -245,7 +249,9 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnGeom g, T* __restr
     qsh[wv][lane] = to_f(q[lane]) / g.temperature;
     for (int c = lane; c < g.Lk * (64 / V); c += 64) {
       const int jj = c / (64 / V), d0 = (c % (64 / V)) * V;
-      *reinterpret_cast<VT*>(&vsh[wv][jj * 64 + d0]) = *reinterpret_cast<const VT*>(vb + (int64_t)jj * g.v_ld + d0);
+      const int64_t roff = g.kv_row ? (int64_t)(g.kv_row[(int64_t)b * g.kv_row_ld + jj] - bk) * g.v_bs : 0;
+      *reinterpret_cast<VT*>(&vsh[wv][jj * 64 + d0]) =
+          *reinterpret_cast<const VT*>(vb + roff + (int64_t)jj * g.v_ld + d0);
     }
   }
   __syncthreads();
@@ -253,7 +259,8 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnGeom g, T* __restr
   const int j = lane;
   float s = -INFINITY;
   if (j < g.Lk && !key_masked(g, b, 0, j)) {
-    const T* kr = kb + (int64_t)j * g.k_ld;
+    const int64_t roff = g.kv_row ? (int64_t)(g.kv_row[(int64_t)b * g.kv_row_ld + j] - bk) * g.k_bs : 0;
+    const T* kr = kb + roff + (int64_t)j * g.k_ld;
     float kx[64];
 #pragma unroll
     for (int d0 = 0; d0 < 64; d0 += V) {
@@ -321,7 +328,7 @@ void attention_fwd(const AttnGeom& g, void* o, float* probs, DType t, hipStream_
     CAPGEN_HIP(hipGetLastError());
     return;
   }
-  if (t == DType::BF16 && attention_mfma_ok(g)) return attention_fwd_mfma(g, (bf16*)o, probs, s);
+  if (t == DType::BF16 && !g.kv_row && attention_mfma_ok(g)) return attention_fwd_mfma(g, (bf16*)o, probs, s);
   const size_t smem = fwd_smem(g);
   require(smem <= 160 * 1024, "attention_fwd: LDS budget exceeded");
   dim3 grid(g.B * g.H);

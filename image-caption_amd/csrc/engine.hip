@@ -113,9 +113,12 @@ struct Acts {
 struct GenWS {
   int R = 0, N = 0;  // capacity (rows, regions)
   void *x, *x1, *x2, *q, *att, *tmp, *h, *E;
-  float *mean, *rstd, *Pc, *logits, *probs;
-  void *cache, *cache2;  // [Ld][R][Tcap][2d]
-  int32_t *ids, *ids2;   // [R][Tcap]
+  float *mean, *rstd, *Pc, *logits;
+  float* cand_v;          // beam: each row's k finalists (beam_step_topk)
+  int32_t* cand_i;
+  void* cache;            // [Ld][R][Tcap][2d]: row r's K/V of position t at [l][r][t]
+  int32_t *ids, *ids2;    // [R][Tcap]
+  int32_t *kvrow, *kvrow2;  // beam: [R][Tcap] row holding the K/V of (beam row, position)
   int64_t *seq, *seq2;   // beam [R][Tw]
   float *bprob, *bprob2;
   int32_t *bsrc, *btok;
@@ -127,87 +130,6 @@ __global__ void init_gen_ids_kernel(int64_t* out, int rows, int width, int32_t* 
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c < rows * width) out[c] = (c % width) == 0 ? 1 : 0;
   if (c < rows * tcap) ids[c] = (c % tcap) == 0 ? 1 : 0;
-}
-
-// one workgroup per image: top-k (descending, lowest index first on ties) over the k*V
-// candidates probs[j*B+i][v] + prob[j][i]   (model.py:183-190).  One pass: every thread keeps a
-// sorted register top-KM of its strided candidates, then the block merges the 256 * KM
-// finalists in LDS (k rounds of a block argmax over <= 4096 entries).  (value desc, index asc)
-// is a strict total order, so the selection equals a full sort's first k.
-template <int KM>
-__global__ void __launch_bounds__(256) beam_topk_kernel(const float* __restrict__ probs, const float* __restrict__ prev,
-                                                        int k_in, int B, int V, int k, float* __restrict__ out_prob,
-                                                        int32_t* __restrict__ out_src, int32_t* __restrict__ out_tok) {
-  __shared__ float fv[256 * KM];
-  __shared__ int fi[256 * KM];
-  __shared__ float bv[4];
-  __shared__ int bi[4], bp[4];
-  const int i = blockIdx.x, tid = threadIdx.x;
-  float tv[KM];
-  int ti[KM];
-#pragma unroll
-  for (int u = 0; u < KM; ++u) tv[u] = -INFINITY, ti[u] = 0x7fffffff;
-  for (int j = 0; j < k_in; ++j) {
-    const float* row = probs + ((int64_t)j * B + i) * V;
-    const float add = prev ? prev[j * B + i] : 0.f;
-    for (int v = tid; v < V; v += 256) {
-      const float x = row[v] + add;
-      const int c = j * V + v;
-      if (!(x > tv[KM - 1] || (x == tv[KM - 1] && c < ti[KM - 1]))) continue;
-      // insert into the sorted register list (unrolled: no dynamic register indexing)
-      float cv = x;
-      int ci = c;
-#pragma unroll
-      for (int u = 0; u < KM; ++u) {
-        const bool better = cv > tv[u] || (cv == tv[u] && ci < ti[u]);
-        const float ov = tv[u];
-        const int oi = ti[u];
-        tv[u] = better ? cv : ov;
-        ti[u] = better ? ci : oi;
-        cv = better ? ov : cv;
-        ci = better ? oi : ci;
-      }
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < KM; ++u) fv[u * 256 + tid] = tv[u], fi[u * 256 + tid] = ti[u];
-  __syncthreads();
-  for (int sel = 0; sel < k; ++sel) {
-    float best = -INFINITY;
-    int bidx = 0x7fffffff, bpos = -1;
-    for (int e = tid; e < 256 * KM; e += 256) {
-      const float x = fv[e];
-      const int c = fi[e];
-      if (x > best || (x == best && c < bidx)) best = x, bidx = c, bpos = e;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(best, o, 64);
-      const int oi = __shfl_xor(bidx, o, 64);
-      const int op = __shfl_xor(bpos, o, 64);
-      if (ov > best || (ov == best && oi < bidx)) best = ov, bidx = oi, bpos = op;
-    }
-    if ((tid & 63) == 0) bv[tid >> 6] = best, bi[tid >> 6] = bidx, bp[tid >> 6] = bpos;
-    __syncthreads();
-    if (tid == 0) {
-      int w0 = 0;
-      for (int w = 1; w < 4; ++w)
-        if (bv[w] > bv[w0] || (bv[w] == bv[w0] && bi[w] < bi[w0])) w0 = w;
-      out_prob[sel * B + i] = bv[w0];
-      out_src[sel * B + i] = bi[w0] / V;
-      out_tok[sel * B + i] = bi[w0] % V;
-      if (bp[w0] >= 0) fv[bp[w0]] = -INFINITY, fi[bp[w0]] = 0x7fffffff;
-    }
-    __syncthreads();
-  }
-}
-
-static void beam_topk(const float* probs, const float* prev, int k_in, int B, int V, int k, float* out_prob,
-                      int32_t* out_src, int32_t* out_tok, hipStream_t s) {
-  if (k <= 4) beam_topk_kernel<4><<<B, 256, 0, s>>>(probs, prev, k_in, B, V, k, out_prob, out_src, out_tok);
-  else if (k <= 8) beam_topk_kernel<8><<<B, 256, 0, s>>>(probs, prev, k_in, B, V, k, out_prob, out_src, out_tok);
-  else beam_topk_kernel<16><<<B, 256, 0, s>>>(probs, prev, k_in, B, V, k, out_prob, out_src, out_tok);
-  CAPGEN_HIP(hipGetLastError());
 }
 
 // dst row r = (j, i) <- src row (src[j][i], i); then optionally set column `col` to tok
@@ -223,15 +145,15 @@ __global__ void beam_gather_kernel(const E* __restrict__ src, E* __restrict__ ds
     d[c] = (tok && c == col) ? (E)tok[r] : s[c];
 }
 
-// the KV-cache rows of beam reorder: 16-B copies (row_elems, copy_elems multiples of 16 B)
-__global__ void beam_gather16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t row_vec,
-                                     int64_t copy_vec, const int32_t* __restrict__ bsrc, int B) {
-  const int r = blockIdx.y;
+// beam reorder of the K/V row table (attention kv_row): row r's positions 0..t come from its
+// source beam's row, position t + 1 (written by row r's own next decoder step) is row r
+__global__ void beam_kvrow_kernel(const int32_t* __restrict__ src, int32_t* __restrict__ dst, int Tc, int t,
+                                  const int32_t* __restrict__ bsrc, int B, int R) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= R * Tc) return;
+  const int r = e / Tc, c = e % Tc;
   const int srow = bsrc[r] * B + (r % B);
-  const uint4* s = src + (int64_t)srow * row_vec;
-  uint4* d = dst + (int64_t)r * row_vec;
-  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < copy_vec; c += (int64_t)gridDim.x * blockDim.x)
-    d[c] = s[c];
+  dst[e] = c <= t ? src[(int64_t)srow * Tc + c] : (c == t + 1 ? r : 0);
 }
 
 }  // namespace
@@ -1480,11 +1402,13 @@ struct capgen_engine {
     p.take(g.rstd, R);
     p.take(g.Pc, (size_t)R * L.Hd * N);
     p.take(g.logits, (size_t)R * L.V);
-    p.take(g.probs, (size_t)R * L.V);
+    p.take(g.cand_v, (size_t)R * 16);
+    p.take(g.cand_i, (size_t)R * 16);
     T_(g.cache, (int64_t)L.Ld * R * Tc * 2 * dd);
-    T_(g.cache2, (int64_t)L.Ld * R * Tc * 2 * dd);
     p.take(g.ids, (size_t)R * Tc);
     p.take(g.ids2, (size_t)R * Tc);
+    p.take(g.kvrow, (size_t)R * Tc);
+    p.take(g.kvrow2, (size_t)R * Tc);
     p.take(g.seq, (size_t)R * Tc);
     p.take(g.seq2, (size_t)R * Tc);
     p.take(g.bprob, R);
@@ -1514,7 +1438,8 @@ struct capgen_engine {
 
   // decoder for position t of R rows (rows r -> image r % Bimg); tokens = ids[:, t].
   // Leaves logits [R, V] in g.logits; cross-attn probs of the last block in g.Pc if want_attn.
-  void dec_step(int R, int Bimg, int N, int t, void* cache, const int32_t* ids, bool want_attn, hipStream_t s) {
+  void dec_step(int R, int Bimg, int N, int t, void* cache, const int32_t* ids, bool want_attn, hipStream_t s,
+                const int32_t* kv_row = nullptr) {
     const int dd = L.dd, Hd = L.Hd, dkd = dd / Hd, Tc = L.maxlen;
     embedding_gather(P(L.emb), ids + t, Tc, R, L.dwe, g.E, act, s);
     linear(g.E, L.dwe, L.Wel, L.dwe, g.tmp, dd, act, R, dd, L.dwe, nullptr, 0, s);
@@ -1528,9 +1453,16 @@ struct capgen_engine {
     for (int l = 0; l < L.Ld; ++l) {
       const auto& w = L.dec[l];
       void* cl = at(cache, (int64_t)l * R * cld);
-      linear(g.x, dd, w.Wqkv, dd, g.q, dd, act, R, dd, dd, nullptr, 0, s);
-      linear(g.x, dd, w.Wqkv + (int64_t)dd * dd, dd, at(cl, (int64_t)t * 2 * dd), cld, act, R, 2 * dd, dd, nullptr, 0,
-             s);
+      if (act == DType::BF16) {  // one GEMM: Q columns -> g.q, K/V columns -> the cache at position t
+        GemmArgs ga;
+        ga.M = R, ga.N = 3 * dd, ga.K = dd, ga.A = g.x, ga.lda = dd, ga.B = W(w.Wqkv), ga.ldb = dd;
+        ga.C = g.q, ga.ldc = dd, ga.C2 = at(cl, (int64_t)t * 2 * dd), ga.ldc2 = cld, ga.nsplit = dd;
+        gemm(ga, act, act, false, false, s);
+      } else {
+        linear(g.x, dd, w.Wqkv, dd, g.q, dd, act, R, dd, dd, nullptr, 0, s);
+        linear(g.x, dd, w.Wqkv + (int64_t)dd * dd, dd, at(cl, (int64_t)t * 2 * dd), cld, act, R, 2 * dd, dd, nullptr,
+               0, s);
+      }
       AttnGeom sg;
       sg.B = R, sg.H = Hd, sg.Lq = 1, sg.Lk = t + 1, sg.dk = dkd;
       sg.q = g.q, sg.q_ld = dd, sg.q_bs = dd;
@@ -1538,6 +1470,7 @@ struct capgen_engine {
       sg.v = at(cl, dd), sg.v_ld = 2 * dd, sg.v_bs = cld;
       sg.o_ld = dd, sg.o_bs = dd;
       sg.key_ids = ids, sg.kid_bs = Tc, sg.pad_idx = cfg.pad_idx, sg.causal = 1, sg.q_pos0 = t;
+      sg.kv_row = kv_row, sg.kv_row_ld = Tc;
       sg.temperature = std::sqrt((float)dkd);
       attf(sg, g.att, nullptr, act, s);
       linear(g.att, dd, w.Wo_s, dd, g.tmp, dd, act, R, dd, dd, nullptr, 0, s);
@@ -1618,32 +1551,28 @@ struct capgen_engine {
     init_gen_ids_kernel<<<(R * Tc + 255) / 256, 256, 0, s>>>(g.seq, R, Tw, g.ids, Tc);
     CAPGEN_HIP(hipGetLastError());
     // position 0: every beam holds <START>; top-k of beam 0's distribution (model.py:148-166)
+    beam_kvrow_kernel<<<(R * Tc + 255) / 256, 256, 0, s>>>(g.kvrow2, g.kvrow, Tc, -1, g.ids, B, R);  // [r][0] = r
     dec_step(R, B, N, 0, g.cache, g.ids, false, s);
-    softmax_rows(g.logits, R, L.V, g.probs, s, decode_logsm);
-    beam_topk(g.probs, nullptr, 1, B, L.V, k, g.bprob, g.bsrc, g.btok, s);
+    beam_step_topk(g.logits, nullptr, 1, B, L.V, k, decode_logsm, g.cand_v, g.cand_i, g.bprob, g.bsrc, g.btok, s);
     CAPGEN_HIP(hipMemsetAsync(g.bsrc, 0, sizeof(int32_t) * R, s));  // all beams descend from beam 0 at t = 0
+    // The K/V cache is never copied: row r writes its position-t K/V at [l][r][t] and reads
+    // position j of its history from row kvrow[r][j] (the beam it descended from there); a
+    // reorder moves only the ids / sequences and this [R][Tc] table
     auto reorder = [&](int t) {
       // seq/ids rows follow their source beam, then column t+1 = chosen token
       dim3 gs(1, R);
       beam_gather_kernel<int64_t><<<gs, 64, 0, s>>>(g.seq, g.seq2, Tw, Tw, g.bsrc, B, R, g.btok, t + 1);
       beam_gather_kernel<int32_t><<<gs, 64, 0, s>>>(g.ids, g.ids2, Tc, Tc, g.bsrc, B, R, g.btok, t + 1);
-      const int64_t cld = (int64_t)Tc * 2 * dd;
-      const int64_t vec_per_row = cld * (int64_t)es_() / 16, copy_vec = (int64_t)(t + 1) * 2 * dd * es_() / 16;
-      for (int l = 0; l < L.Ld; ++l) {
-        dim3 gc((unsigned)std::min<int64_t>((copy_vec + 255) / 256, 64), R);
-        beam_gather16_kernel<<<gc, 256, 0, s>>>((const uint4*)at(g.cache, l * R * cld), (uint4*)at(g.cache2, l * R * cld),
-                                                vec_per_row, copy_vec, g.bsrc, B);
-      }
+      beam_kvrow_kernel<<<(R * Tc + 255) / 256, 256, 0, s>>>(g.kvrow, g.kvrow2, Tc, t, g.bsrc, B, R);
       CAPGEN_HIP(hipGetLastError());
       std::swap(g.seq, g.seq2);
       std::swap(g.ids, g.ids2);
-      std::swap(g.cache, g.cache2);
+      std::swap(g.kvrow, g.kvrow2);
     };
     reorder(0);
     for (int t = 1; t < Tw - 1; ++t) {
-      dec_step(R, B, N, t, g.cache, g.ids, false, s);
-      softmax_rows(g.logits, R, L.V, g.probs, s, decode_logsm);
-      beam_topk(g.probs, g.bprob, k, B, L.V, k, g.bprob2, g.bsrc, g.btok, s);
+      dec_step(R, B, N, t, g.cache, g.ids, false, s, g.kvrow);
+      beam_step_topk(g.logits, g.bprob, k, B, L.V, k, decode_logsm, g.cand_v, g.cand_i, g.bprob2, g.bsrc, g.btok, s);
       std::swap(g.bprob, g.bprob2);
       reorder(t);
     }

@@ -25,6 +25,9 @@ struct GemmArgs {
   int prio = 0;                      // 1: critical-path launch, waves raise their issue priority
   const float* cin = nullptr;        // += cin[m][n] (f32, row stride ldcin) before the activation
   int64_t ldcin = 0;
+  void* C2 = nullptr;                // bf16 path: columns n >= nsplit go to C2[m][n - nsplit] (row
+  int64_t ldc2 = 0;                  //   stride ldc2), e.g. Q to one buffer and K/V to a cache
+  int nsplit = 0;                    //   (nsplit % 4 == 0)
   int relu = 0;
   float* colsum = nullptr;           // += column sums of the (post-epilogue, beta=0) output, f32 [N]
   int colsum_stripes = 1;            // workgroup w adds into colsum + (w % stripes) * colsum_stride

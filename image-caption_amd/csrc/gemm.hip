@@ -222,6 +222,8 @@ void gemm(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t 
   require(g.K > 0, "gemm: K must be positive");
   require(!g.colsum || !g.beta, "gemm: colsum requires beta == 0");
   require(!g.cin || in == DType::BF16, "gemm: cin is a bf16-path epilogue input");
+  require(!g.C2 || (in == DType::BF16 && g.nsplit % 4 == 0 && !g.beta && !g.colsum),
+          "gemm: a split output (C2) needs the bf16 path, nsplit % 4 == 0, no beta / colsum");
   if (in == DType::F32) {
     if (out == DType::F32) launch_layout<float, float>(g, ta, tb, s);
     else launch_layout<float, bf16>(g, ta, tb, s);

@@ -382,6 +382,7 @@ template <typename TO, int FM, int FN, int TM, int TN>
 __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&acc)[FM][FN], int m0, int n0, int wm,
                                               int wn, int lane, float alpha) {
   TO* __restrict__ C = reinterpret_cast<TO*>(g.C);
+  TO* __restrict__ C2 = reinterpret_cast<TO*>(g.C2);
   const bf16* __restrict__ aux = reinterpret_cast<const bf16*>(g.aux);
   const int fr = lane & 15, fq = lane >> 4;
 #pragma unroll
@@ -389,6 +390,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&a
     const int n = n0 + wn * TN + j * 16 + fq * 4;
     float cs[4] = {0.f, 0.f, 0.f, 0.f};
     if (n >= g.N) continue;
+    const bool hi = C2 && n >= g.nsplit;  // split output: this 4-column group goes to C2
     float bn[4] = {0.f, 0.f, 0.f, 0.f};
     if (g.bias) {
       float4 b4 = *reinterpret_cast<const float4*>(g.bias + n);
@@ -417,7 +419,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&a
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
       }
-      TO* cp = C + (int64_t)m * g.ldc + n;
+      TO* cp = hi ? C2 + (int64_t)m * g.ldc2 + (n - g.nsplit) : C + (int64_t)m * g.ldc + n;
       if (g.beta) {
         float o[4];
         load4<TO>(cp, o);
@@ -673,7 +675,8 @@ static Choice tune(const GemmArgs& g, hipStream_t s) {
   CAPGEN_HIP(hipGetDevice(&dev));
   GemmArgs t = g;
   void* scratch = nullptr;
-  CAPGEN_HIP(hipMalloc(&scratch, (size_t)g.M * g.ldc * sizeof(TO)));
+  if (t.C2) t.C2 = nullptr, t.nsplit = 0, t.ldc = std::max<int64_t>(t.ldc, t.N);  // all columns to scratch
+  CAPGEN_HIP(hipMalloc(&scratch, (size_t)t.M * t.ldc * sizeof(TO)));
   t.C = scratch;
   t.beta = 0;
   t.colsum = nullptr;

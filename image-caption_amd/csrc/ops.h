@@ -82,8 +82,11 @@ void to_bf16(const float* src, bf16* dst, size_t n, hipStream_t s);
 // greedy: out token = argmax(softmax(logits[b])) (first index on ties)   (model.py:126-128)
 void argmax_softmax(const float* logits, int B, int V, int64_t* ids_out, int64_t ids_ld, int col,
                     int32_t* next_ids, int64_t next_ld, hipStream_t s, int logsm = 0);
-// softmax probabilities [B][V] (for beam search)
-void softmax_rows(const float* logits, int B, int V, float* probs, hipStream_t s, int logsm = 0);
+// one beam-search step (model.py:183-190): rows j*B + i (j < k_in) of logits [k_in*B][V]; the
+// k best (prev[j*B+i] + softmax or log-softmax (logsm) of row j*B+i at v) per image i ->
+// out_prob/src/tok[sel*B + i]; cand_v/cand_i: k_in*B*k scratch (each row's k finalists)
+void beam_step_topk(const float* logits, const float* prev, int k_in, int B, int V, int k, int logsm, float* cand_v,
+                    int32_t* cand_i, float* out_prob, int32_t* out_src, int32_t* out_tok, hipStream_t s);
 void bump_seed(uint64_t* seed, hipStream_t s);
 
 }  // namespace capgen

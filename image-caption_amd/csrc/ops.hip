@@ -678,27 +678,174 @@ void argmax_softmax(const float* logits, int B, int V, int64_t* ids_out, int64_t
   CAPGEN_HIP(hipGetLastError());
 }
 
-__global__ void __launch_bounds__(256) softmax_rows_kernel(const float* __restrict__ logits, int V,
-                                                           float* __restrict__ probs, int logsm) {
-  __shared__ float sh[4];
-  const int b = blockIdx.x;
-  const float* x = logits + (int64_t)b * V;
-  float* y = probs + (int64_t)b * V;
-  float mx = -INFINITY;
-  for (int c = threadIdx.x; c < V; c += 256) mx = fmaxf(mx, x[c]);
-  mx = block_max(mx, sh);
-  float se = 0.f;
-  for (int c = threadIdx.x; c < V; c += 256) se += expf(x[c] - mx);
-  se = block_sum(se, sh);
-  if (logsm) {  // LogSoftmax (model_RL.py:72): (x - max) - log(sum exp)
-    const float lse = logf(se);
-    for (int c = threadIdx.x; c < V; c += 256) y[c] = (x[c] - mx) - lse;
-  } else {
-    for (int c = threadIdx.x; c < V; c += 256) y[c] = expf(x[c] - mx) / se;
+// ---- beam search step (model.py:183-190; PolicyNetwork model_RL.py:182-190 with logsm) ----
+// Candidate (j, v) of image i scores prev[j][i] + p[j*B+i][v] (p: Softmax, or LogSoftmax with
+// logsm); the k best under (score desc, flat index j*V + v asc) -- a strict total order, so the
+// selection equals a full sort's first k.  Part 1, one workgroup per decoder row r = j*B + i:
+// the row's softmax exactly as a separate softmax pass would compute it (same strided
+// per-thread order and block reductions: the scores are bit-identical), the row held in
+// registers (NV values per thread; NV = 0 re-reads it from memory), each thread's sorted
+// top-KM, and the row's top k.  Part 2, one wave per image: top k of its k_in rows' k
+// finalists each -- every image-level winner is in its row's top k.  Neither the [R, V]
+// probabilities nor a [B, k*V] scan exist: one read of the logits per step.
+
+// sorted (desc) register top-KM insert of candidate (x, c)
+template <int KM>
+__device__ __forceinline__ void topk_insert(float (&tv)[KM], int (&ti)[KM], float x, int c) {
+  if (!(x > tv[KM - 1] || (x == tv[KM - 1] && c < ti[KM - 1]))) return;
+  float cv = x;
+  int ci = c;
+#pragma unroll
+  for (int u = 0; u < KM; ++u) {  // unrolled: no dynamic register indexing
+    const bool better = cv > tv[u] || (cv == tv[u] && ci < ti[u]);
+    const float ov = tv[u];
+    const int oi = ti[u];
+    tv[u] = better ? cv : ov;
+    ti[u] = better ? ci : oi;
+    cv = better ? ov : cv;
+    ci = better ? oi : ci;
   }
 }
-void softmax_rows(const float* logits, int B, int V, float* probs, hipStream_t s, int logsm) {
-  softmax_rows_kernel<<<B, 256, 0, s>>>(logits, V, probs, logsm);
+
+// (value, index) winner of a wave: value desc, index asc; pos rides along
+__device__ __forceinline__ void wave_best(float& best, int& bidx, int& bpos) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bidx, o, 64);
+    const int op = __shfl_xor(bpos, o, 64);
+    if (ov > best || (ov == best && oi < bidx)) best = ov, bidx = oi, bpos = op;
+  }
+}
+
+template <int KM, int NV>
+__global__ void __launch_bounds__(256) beam_row_topk_kernel(const float* __restrict__ logits,
+                                                            const float* __restrict__ prev, int B, int V, int k,
+                                                            int logsm, float* __restrict__ cand_v,
+                                                            int* __restrict__ cand_i) {
+  __shared__ float sh[4];
+  __shared__ float wv[4][16];
+  __shared__ int wi[4][16];
+  const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = r / B;
+  const float* x = logits + (int64_t)r * V;
+  float xr[NV > 0 ? NV : 1];
+  float mx = -INFINITY;
+  if constexpr (NV > 0) {
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int c = tid + 256 * u;
+      xr[u] = c < V ? x[c] : -INFINITY;
+      mx = fmaxf(mx, xr[u]);
+    }
+  } else {
+    for (int c = tid; c < V; c += 256) mx = fmaxf(mx, x[c]);
+  }
+  mx = block_max(mx, sh);
+  float se = 0.f;
+  if constexpr (NV > 0) {
+#pragma unroll
+    for (int u = 0; u < NV; ++u)
+      if (tid + 256 * u < V) {
+        const float e = expf(xr[u] - mx);
+        se += e;
+        if (!logsm) xr[u] = e;  // Softmax scores need only exp(x - max)
+      }
+  } else {
+    for (int c = tid; c < V; c += 256) se += expf(x[c] - mx);
+  }
+  se = block_sum(se, sh);
+  const float lse = logf(se), add = prev ? prev[r] : 0.f;
+  float tv[KM];
+  int ti[KM];
+#pragma unroll
+  for (int u = 0; u < KM; ++u) tv[u] = -INFINITY, ti[u] = 0x7fffffff;
+  if constexpr (NV > 0) {
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int c = tid + 256 * u;
+      if (c < V) topk_insert<KM>(tv, ti, (logsm ? (xr[u] - mx) - lse : xr[u] / se) + add, j * V + c);
+    }
+  } else {
+    for (int c = tid; c < V; c += 256)
+      topk_insert<KM>(tv, ti, (logsm ? (x[c] - mx) - lse : expf(x[c] - mx) / se) + add, j * V + c);
+  }
+  // the row's k best: k rounds of a wave argmax over the lanes' list heads (the winner pops its
+  // head) give each wave's k best; wave 0 then selects the row's k from the 4 k of them
+  for (int sel = 0; sel < k; ++sel) {
+    float best = tv[0];
+    int bidx = ti[0], bpos = lane;
+    wave_best(best, bidx, bpos);
+    if (lane == 0) wv[wave][sel] = best, wi[wave][sel] = bidx;
+    if (lane == bpos) {
+#pragma unroll
+      for (int u = 0; u + 1 < KM; ++u) tv[u] = tv[u + 1], ti[u] = ti[u + 1];
+      tv[KM - 1] = -INFINITY, ti[KM - 1] = 0x7fffffff;
+    }
+  }
+  __syncthreads();
+  if (wave == 0) {
+    const bool on = lane < 4 * k;
+    float v = on ? wv[lane / k][lane % k] : -INFINITY;
+    int c = on ? wi[lane / k][lane % k] : 0x7fffffff;
+    for (int sel = 0; sel < k; ++sel) {
+      float best = v;
+      int bidx = c, bpos = lane;
+      wave_best(best, bidx, bpos);
+      if (lane == 0) cand_v[(int64_t)r * k + sel] = best, cand_i[(int64_t)r * k + sel] = bidx;
+      if (lane == bpos) v = -INFINITY, c = 0x7fffffff;
+    }
+  }
+}
+
+// one wave per image: the k best of its k_in * k row finalists (k_in * k <= 256)
+__global__ void __launch_bounds__(64) beam_merge_kernel(const float* __restrict__ cand_v, const int* __restrict__ cand_i,
+                                                        int k_in, int B, int V, int k, float* __restrict__ out_prob,
+                                                        int32_t* __restrict__ out_src, int32_t* __restrict__ out_tok) {
+  const int i = blockIdx.x, lane = threadIdx.x, n = k_in * k;
+  float v[4];
+  int c[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = lane + 64 * u;  // entry e = (row j = e / k, rank e % k)
+    const bool on = e < n;
+    const int64_t src = ((int64_t)(e / k) * B + i) * k + e % k;
+    v[u] = on ? cand_v[src] : -INFINITY;
+    c[u] = on ? cand_i[src] : 0x7fffffff;
+  }
+  for (int sel = 0; sel < k; ++sel) {
+    float best = -INFINITY;
+    int bidx = 0x7fffffff, bpos = -1;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (v[u] > best || (v[u] == best && c[u] < bidx)) best = v[u], bidx = c[u], bpos = lane + 64 * u;
+    wave_best(best, bidx, bpos);
+    if (lane == 0) {
+      out_prob[sel * B + i] = best;
+      out_src[sel * B + i] = bidx / V;
+      out_tok[sel * B + i] = bidx % V;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (bpos == lane + 64 * u) v[u] = -INFINITY, c[u] = 0x7fffffff;
+  }
+}
+
+template <int KM>
+static void beam_row_topk(const float* logits, const float* prev, int rows, int B, int V, int k, int logsm,
+                          float* cand_v, int32_t* cand_i, hipStream_t s) {
+  if (V <= 256 * 40) beam_row_topk_kernel<KM, 40><<<rows, 256, 0, s>>>(logits, prev, B, V, k, logsm, cand_v, cand_i);
+  else beam_row_topk_kernel<KM, 0><<<rows, 256, 0, s>>>(logits, prev, B, V, k, logsm, cand_v, cand_i);
+}
+
+void beam_step_topk(const float* logits, const float* prev, int k_in, int B, int V, int k, int logsm, float* cand_v,
+                    int32_t* cand_i, float* out_prob, int32_t* out_src, int32_t* out_tok, hipStream_t s) {
+  require(k >= 1 && k <= 16 && k_in >= 1 && k_in * k <= 256, "beam_step_topk: k in [1, 16]");
+  const int rows = k_in * B;
+  if (k <= 4) beam_row_topk<4>(logits, prev, rows, B, V, k, logsm, cand_v, cand_i, s);
+  else if (k == 5) beam_row_topk<5>(logits, prev, rows, B, V, k, logsm, cand_v, cand_i, s);
+  else if (k <= 8) beam_row_topk<8>(logits, prev, rows, B, V, k, logsm, cand_v, cand_i, s);
+  else beam_row_topk<16>(logits, prev, rows, B, V, k, logsm, cand_v, cand_i, s);
+  beam_merge_kernel<<<B, 64, 0, s>>>(cand_v, cand_i, k_in, B, V, k, out_prob, out_src, out_tok);
   CAPGEN_HIP(hipGetLastError());
 }
 

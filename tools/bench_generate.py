@@ -27,6 +27,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--modes", default="beam5,greedy")
     args = ap.parse_args()
     cfg = preset("C2", dtype="bf16")
     dev = torch.device("cuda", 0)
@@ -40,6 +41,8 @@ def main():
     p = p.to(dev).contiguous()
     runs = {"beam5": lambda: eng.beam(f, p, 5), "greedy": lambda: eng.greedy(f, p, want_attention=False)}
     for name, fn in runs.items():
+        if name not in args.modes.split(","):
+            continue
         fn()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
