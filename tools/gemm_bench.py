@@ -154,3 +154,7 @@ if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "matrix2":
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "matrix":
     matrix([(2304, 512, 2048, 0, 1, 0), (2304, 2048, 512, 0, 0, 0), (2304, 512, 512, 0, 0, 0),
             (1216, 512, 2048, 0, 1, 0), (2304, 1536, 512, 0, 0, 0)])
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "matrix3":
+    # decoder-side shapes (M = 64 x 19 = 1216 rows)
+    matrix([(1216, 512, 2048, 0, 0, 0), (1216, 512, 2048, 0, 1, 0), (1216, 2048, 512, 0, 1, 0),
+            (1216, 512, 512, 0, 0, 0), (1216, 512, 512, 0, 1, 0)], sks=(1, 2, 3, 4))
