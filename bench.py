@@ -152,6 +152,7 @@ def main():
     ap.add_argument("--graph", action="store_true", help="replay the step as one hipGraph (slower on ROCm 7)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=5)
+    ap.add_argument("--no-host-batches", action="store_true", help="skip the secondary host-batch line")
     args = ap.parse_args()
 
     from capgen import preset
@@ -240,7 +241,8 @@ def main():
     }
     if rank == 0 and world == 1:
         out["dominant_kernel"] = dominant_gemm(eng)
-        out["host_batches"] = host_batches(eng, cfg, dev)
+        if not args.no_host_batches:
+            out["host_batches"] = host_batches(eng, cfg, dev)
         if not args.no_cpu_baseline:
             del eng
             torch.cuda.empty_cache()

@@ -256,7 +256,16 @@ struct capgen_engine {
     const char* e = std::getenv("CAPGEN_PRIO");
     return !(e && e[0] == '0');
   }();
-  int prio(hipStream_t s) const { return prio_on && s == es && es2 != es ? 1 : 0; }
+  hipStream_t crit = nullptr;  // critical stream of the running call (es, or the caller's: direct)
+  int prio(hipStream_t s) const { return prio_on && s == (crit ? crit : es) && es2 != s ? 1 : 0; }
+  // direct steps (CAPGEN_DIRECT, default on): once the forward graph exists, train_step runs its
+  // critical path on the CALLER's stream -- no caller -> engine -> caller event round trip per
+  // step; es then waits for the step so the engine's host-side syncs on es still cover it
+  // (measured: 3.165 vs 3.170 ms/step, within noise -- the step-boundary gap is the Adam tail)
+  bool direct_on = [] {
+    const char* e = std::getenv("CAPGEN_DIRECT");
+    return !(e && e[0] == '0');
+  }();
 
   // the row / attention kernels with the launch's issue priority (prio above)
   void lnf(LnFwd l, hipStream_t s) const {
@@ -1207,8 +1216,18 @@ struct capgen_engine {
   void train_step(const void* f, DType ft, const float* pos, const int32_t* caps, int B, int N, int T, float* loss,
                   hipStream_t cs) {
     ensure_acts(B, N, T);
-    enter(cs);
     Key k{f, pos, caps, loss, (int)ft, B, N, T, training, in_idx, in_n_img};
+    if (direct_on && !graph_on && fwd_graph_on && !comm && fexec && fkey == k && cs != es) {
+      crit = cs;
+      CAPGEN_HIP(hipGraphLaunch(fexec, cs));
+      fB = B, fN = N, fT = T, fwd_drop = training;  // host state forward() would have set
+      backward(cs, /*step_params=*/true);
+      crit = nullptr;
+      CAPGEN_HIP(hipEventRecord(ev_out, cs));
+      CAPGEN_HIP(hipStreamWaitEvent(es, ev_out, 0));
+      return;
+    }
+    enter(cs);
     auto body = [&]() {
       static const bool host_timing = std::getenv("CAPGEN_HOST_TIMING") != nullptr;  // diagnostic
       static double tf = 0, tb = 0;

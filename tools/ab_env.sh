@@ -6,7 +6,7 @@ var=$1; shift
 mkdir -p gpurun_out
 for round in 1 2; do
   for v in "$@"; do
-    env "$var=$v" timeout -k 10 120 python -u bench.py --steps 100 --no-cpu-baseline > gpurun_out/ab.json 2> gpurun_out/ab.err \
+    env "$var=$v" timeout -k 10 120 python -u bench.py --steps 100 --no-cpu-baseline --no-host-batches > gpurun_out/ab.json 2> gpurun_out/ab.err \
       || { tail -20 gpurun_out/ab.err; exit 1; }
     python3 -c "import json,sys; d=json.load(open('gpurun_out/ab.json')); print('$var=$v', d['ms_per_step'], d['roofline']['scope'].split('step time ')[1][:10])"
   done
