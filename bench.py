@@ -203,6 +203,7 @@ def main():
     for _ in range(args.steps):
         eng.train_step_raw(f, ft, p, c, B, N, T, loss)
     ev1.record(stream)
+    issue_s = time.perf_counter() - t0  # host time to enqueue the K steps (no sync inside)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -238,6 +239,9 @@ def main():
                                                          f"summary {traffic['source']} (not measured in this run)"
                                                          if traffic else "")},
         "final_loss": round(final_loss, 5),
+        # diagnostic: host enqueue time per step; close to ms_per_step means the host issue rate,
+        # not the GPU, sets the step time
+        "host_issue_ms_per_step": round(issue_s / args.steps * 1e3, 4),
     }
     if rank == 0 and world == 1:
         out["dominant_kernel"] = dominant_gemm(eng)

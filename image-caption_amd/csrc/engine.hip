@@ -86,6 +86,8 @@ struct Acts {
   std::vector<DecAct> dec;
   float* logits;
   void* dlogits;
+  float2* ce_stats;  // fused classifier + CE (bf16): {max, sum exp} per row and 16-column slab
+  float* ce_tl;      // its target logits
   float *loss_row, *grad_scale, *loss, *loss_ce;
   float* gEnc32;  // f32 partial sum of the encoder-output gradient over decoder blocks Ld-1 .. 1
   // SCST (rl.hip): per-row sample / lse / logp[sample] / entropy, per-image entropy, scalars
@@ -262,6 +264,13 @@ struct capgen_engine {
   // critical path on the CALLER's stream -- no caller -> engine -> caller event round trip per
   // step; es then waits for the step so the engine's host-side syncs on es still cover it
   // (measured: 3.165 vs 3.170 ms/step, within noise -- the step-boundary gap is the Adam tail)
+  // fused classifier + cross entropy in the bf16 path (CAPGEN_FUSED_CE=0: logits in f32 + ce_kernel)
+  bool fused_ce_on = [] {
+    const char* e = std::getenv("CAPGEN_FUSED_CE");
+    return !(e && e[0] == '0');
+  }();
+  bool need_logits = false;  // the next forward must materialise the f32 logits (SCST sampling)
+  bool fused_ce() const { return fused_ce_on && !need_logits && act == DType::BF16 && L_().V % 4 == 0; }
   bool direct_on = [] {
     const char* e = std::getenv("CAPGEN_DIRECT");
     return !(e && e[0] == '0');
@@ -399,6 +408,8 @@ struct capgen_engine {
     }
     p.take(a.logits, Md * L_().V);
     T_(a.dlogits, Md * L_().V);
+    a.ce_stats = reinterpret_cast<float2*>(p.raw((size_t)Md * ((L_().V + 15) / 16) * sizeof(float2)));
+    p.take(a.ce_tl, Md);
     p.take(a.loss_row, Md);
     p.take(a.grad_scale, 4);
     p.take(a.loss, 4);
@@ -747,8 +758,20 @@ struct capgen_engine {
     if (L.has_mf)
       move_first_fwd(a.D[L.Ld], a.X[L.Le], Md, Lq, 0, N, a.mfU, a.mfH, a.tmp, a.mfOut, a.mfV, a.mfM, a.mfR, drop_on, s);
     // ---- classifier + CE (model.py:93-96) ----
-    linear(dec_out(), dd, L.Wc, dd, a.logits, L.V, DType::F32, Md, L.V, dd, P(L.bc), 0, s);
-    cross_entropy_rows(a.logits, a.tgt, Md, L.V, cfg.pad_idx, a.loss_row, a.dlogits, act, s);
+    if (fused_ce()) {
+      // the logits are never written: the GEMM epilogue leaves exp(v - slab max) + slab stats,
+      // ce_finish turns them into the loss rows and softmax - onehot (model.py:93-96)
+      GemmArgs ga;
+      ga.M = Md, ga.N = L.V, ga.K = dd, ga.A = dec_out(), ga.lda = dd, ga.B = W(L.Wc), ga.ldb = dd;
+      ga.C = a.dlogits, ga.ldc = L.V, ga.bias = P(L.bc), ga.prio = prio(s);
+      ga.ce_stats = a.ce_stats, ga.ce_ld = (L.V + 15) / 16, ga.ce_tgt = a.tgt, ga.ce_tlogit = a.ce_tl;
+      gemm(ga, act, act, false, false, s);
+      ce_finish(a.ce_stats, (L.V + 15) / 16, a.ce_tl, a.tgt, Md, L.V, cfg.pad_idx, a.loss_row,
+                reinterpret_cast<bf16*>(a.dlogits), s);
+    } else {
+      linear(dec_out(), dd, L.Wc, dd, a.logits, L.V, DType::F32, Md, L.V, dd, P(L.bc), 0, s);
+      cross_entropy_rows(a.logits, a.tgt, Md, L.V, cfg.pad_idx, a.loss_row, a.dlogits, act, s);
+    }
     float* lo = loss_out ? loss_out : a.loss;
     if (comm) {
       // data parallel: the mean CE over the GLOBAL batch (model.py:76) is the sum of the ranks'
@@ -967,8 +990,6 @@ struct capgen_engine {
     dbg_snap_on = layer == L.Le - 1;
     if (dbg_stop == 4 && dbg_snap_on && !dbg_snap[0])
       for (void*& q : dbg_snap) CAPGEN_HIP(hipMalloc(&q, (size_t)Me * d * es_()));
-    mha_out_bwd(Me, d, lmha, A.att, w.Wo, gb.gATT1, s);
-    dbg_snap_on = false;
     AttnGeom g;
     g.B = B, g.H = He, g.Lq = N, g.Lk = N, g.dk = dke;
     g.q = A.qkv, g.q_ld = 3 * d, g.q_bs = (int64_t)N * 3 * d;
@@ -978,6 +999,8 @@ struct capgen_engine {
     if (valid) g.key_valid = valid, g.kv_bs = N, g.causal = 1;
     g.temperature = std::sqrt((float)dke);
     g.drop = mk_drop(pa, site(0, layer, 0), on);
+    mha_out_bwd(Me, d, lmha, A.att, w.Wo, gb.gATT1, s);
+    dbg_snap_on = false;
     attb(g, A.P, gb.gATT1, gb.gQKV, at(gb.gQKV, d), at(gb.gQKV, 2 * d), act, s);
     dw_side(gb.gQKV, 3 * d, X, d, w.Wqkv, d, Me, 3 * d, d, nullptr, s);
     linear_dx(gb.gQKV, 3 * d, w.Wqkv, d, gO, d, Me, 3 * d, d, 1, nullptr, nullptr, s);  // gO = grad wrt X
@@ -1076,7 +1099,6 @@ struct capgen_engine {
       auto& gb = a.gdec[l];
       const LnBwd lffn = dec_ffn_lb(l, gO, gR), lcross = dec_cross_lb(l, gR, gO), lself = dec_self_lb(l, gO, gR);
       ffn_bwd(Md, dd, L.fd, lffn, A.D2, A.H, w.W1, w.b1, w.W2, gb.gH, s);  // gR = grad wrt D2
-      mha_out_bwd(Md, dd, lcross, A.attc, w.Wo_c, gb.gATT2, s);            // gO = grad wrt D1 (residual part)
       AttnGeom c;
       c.B = B, c.H = Hd, c.Lq = Lq, c.Lk = N, c.dk = dkd;
       c.q = A.qc, c.q_ld = dd, c.q_bs = (int64_t)Lq * dd;
@@ -1086,6 +1108,7 @@ struct capgen_engine {
       c.key_valid = a.valid, c.kv_bs = N;  // masks as in forward (the MFMA backward recomputes P)
       c.temperature = std::sqrt((float)dkd);
       c.drop = mk_drop(pa, site(1, l, 5), on);
+      mha_out_bwd(Md, dd, lcross, A.attc, w.Wo_c, gb.gATT2, s);  // gO = grad wrt D1 (residual part)
       attb(c, A.Pc, gb.gATT2, gb.gQc, at(a.gKV, (int64_t)l * 2 * dd), at(a.gKV, (int64_t)l * 2 * dd + dd), act, s);
       if (split_kv) {  // this block's cross K/V: weight gradient and (l >= 1) encoder-output term
         dw_side(at(a.gKV, (int64_t)l * 2 * dd), kvld, a.X[L.Le], d, L.Wkv_all + (int64_t)l * 2 * dd * d, d, Me,
@@ -1097,7 +1120,6 @@ struct capgen_engine {
       }
       dw_side(gb.gQc, dd, A.D1, dd, w.Wq_c, dd, Md, dd, dd, nullptr, s);
       linear_dx(gb.gQc, dd, w.Wq_c, dd, gO, dd, Md, dd, dd, 1, nullptr, nullptr, s);  // gO = grad wrt D1
-      mha_out_bwd(Md, dd, lself, A.atts, w.Wo_s, gb.gATT1, s);  // gR = grad wrt D_l (residual part)
       AttnGeom g;
       g.B = B, g.H = Hd, g.Lq = Lq, g.Lk = Lq, g.dk = dkd;
       g.q = A.qkv, g.q_ld = 3 * dd, g.q_bs = (int64_t)Lq * 3 * dd;
@@ -1107,6 +1129,7 @@ struct capgen_engine {
       g.key_ids = a.ids, g.kid_bs = Lq, g.pad_idx = cfg.pad_idx, g.causal = 1;  // as in forward
       g.temperature = std::sqrt((float)dkd);
       g.drop = mk_drop(pa, site(1, l, 3), on);
+      mha_out_bwd(Md, dd, lself, A.atts, w.Wo_s, gb.gATT1, s);  // gR = grad wrt D_l (residual part)
       attb(g, A.Ps, gb.gATT1, gb.gQKV, at(gb.gQKV, dd), at(gb.gQKV, 2 * dd), act, s);
       dw_side(gb.gQKV, 3 * dd, a.D[l], dd, w.Wqkv, dd, Md, 3 * dd, dd, nullptr, s);
       linear_dx(gb.gQKV, 3 * dd, w.Wqkv, dd, gR, dd, Md, 3 * dd, dd, 1, nullptr, nullptr, s);
@@ -1331,7 +1354,9 @@ struct capgen_engine {
     ensure_acts(B, N, T);
     enter(cs);
     const int Lq = T - 1, Md = B * Lq;
+    need_logits = true;  // rl_rows samples from the logits
     forward(f, ft, pos, caps, B, N, T, nullptr, training, es);
+    need_logits = false;
     rl_rows(a.logits, Md, L.V, a.rl_sample, a.rl_lse, a.rl_logp, a.rl_ent, es);
     rl_image(a.rl_sample, a.rl_ent, B, Lq, a.rl_ent_img, a.rl_scal, es);
     if (sample_out) rl_export(a.rl_sample, Md, sample_out, es);
@@ -1903,6 +1928,9 @@ int capgen_copy_logits(capgen_t* h, float* dst, int64_t n, void* stream) {
     require(n == want, "copy_logits: size mismatch");
     hipStream_t cs = (hipStream_t)stream;
     h->enter(cs);
+    if (h->fused_ce())  // the fused step never writes the logits: recompute them (test hook)
+      h->linear(h->dec_out(), h->L.dd, h->L.Wc, h->L.dd, h->a.logits, h->L.V, DType::F32, h->fB * (h->fT - 1),
+                h->L.V, h->L.dd, h->P(h->L.bc), 0, h->es);
     CAPGEN_HIP(hipMemcpyAsync(dst, h->a.logits, n * 4, hipMemcpyDeviceToDevice, h->es));
     h->leave(cs);
   });

@@ -32,6 +32,14 @@ struct GemmArgs {
   float* colsum = nullptr;           // += column sums of the (post-epilogue, beta=0) output, f32 [N]
   int colsum_stripes = 1;            // workgroup w adds into colsum + (w % stripes) * colsum_stride
   int64_t colsum_stride = 0;
+  // fused cross-entropy epilogue (bf16 NT path only; classifier + CE, model.py:93-96): per row m
+  // and 16-column slab c, v = alpha * acc + bias, mx = max(v), C[m][n] = exp(v - mx) (bf16) and
+  // ce_stats[m * ce_ld + c] = {mx, sum exp(v - mx)}; ce_tlogit[m] = v[ce_tgt[m]] (f32).  The
+  // logits themselves are never written; ce_finish() turns C into softmax - onehot in place.
+  float2* ce_stats = nullptr;
+  int64_t ce_ld = 0;
+  const int32_t* ce_tgt = nullptr;
+  float* ce_tlogit = nullptr;
 };
 
 // Independent GEMMs of one layout launched as ONE grid (tiles problem after problem).

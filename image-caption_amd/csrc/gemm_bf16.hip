@@ -385,6 +385,47 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&a
   TO* __restrict__ C2 = reinterpret_cast<TO*>(g.C2);
   const bf16* __restrict__ aux = reinterpret_cast<const bf16*>(g.aux);
   const int fr = lane & 15, fq = lane >> 4;
+  if constexpr (sizeof(TO) == 2) {
+    if (g.ce_stats) {  // fused cross-entropy epilogue (GemmArgs::ce_stats)
+      // a 16x16 fragment = 16 rows x one 16-column slab; the 4 lanes of a row (lane groups fq)
+      // hold its 4 column quads, so slab max / sum are two xor-shuffles.  Every lane runs the
+      // shuffles (partners share the row, so out-of-range rows only predicate the stores).
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int m = m0 + wm * TM + i * 16 + fr;
+        const bool mok = m < g.M;
+        const int tg = mok ? g.ce_tgt[m] : -1;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int nb = n0 + wn * TN + j * 16, n = nb + fq * 4;
+          const bool nok = n < g.N;
+          float v[4], mx = -INFINITY;
+          if (nok) {
+            const float4 b4 = g.bias ? *reinterpret_cast<const float4*>(g.bias + n) : float4{0.f, 0.f, 0.f, 0.f};
+            v[0] = alpha * acc[i][j][0] + b4.x, v[1] = alpha * acc[i][j][1] + b4.y;
+            v[2] = alpha * acc[i][j][2] + b4.z, v[3] = alpha * acc[i][j][3] + b4.w;
+            mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+          }
+          mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+          mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+          float e[4], sum = 0.f;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            e[r] = nok ? __expf(v[r] - mx) : 0.f;
+            sum += e[r];
+          }
+          sum += __shfl_xor(sum, 16, 64);
+          sum += __shfl_xor(sum, 32, 64);
+          if (mok && nok) {
+            store4<TO>(C + (int64_t)m * g.ldc + n, e);
+            if (tg >= n && tg < n + 4) g.ce_tlogit[m] = v[tg - n];
+          }
+          if (mok && fq == 0 && nb < g.N) g.ce_stats[(int64_t)m * g.ce_ld + nb / 16] = float2{mx, sum};
+        }
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int n = n0 + wn * TN + j * 16 + fq * 4;
@@ -965,6 +1006,9 @@ void gemm_bf16(const GemmArgs& g, DType out, bool ta, bool tb, hipStream_t s) {
   // read-modify-write epilogue: every 128-B line of C must belong to one tile (whole_lines)
   require(!g.beta || (((uintptr_t)g.C & 127) == 0 && (g.ldc * (int64_t)dsize(out)) % 128 == 0),
           "gemm(bf16): beta=1 needs C rows 128-B aligned (one writer per cache line)");
+  require(!g.ce_stats || (out == DType::BF16 && !ta && !tb && !g.beta && !g.C2 && !g.aux && !g.relu && !g.colsum &&
+                          !g.cin && g.ce_tgt && g.ce_tlogit && g.ce_ld >= (g.N + 15) / 16),
+          "gemm(bf16): the fused cross-entropy epilogue is a plain bf16 NT GEMM (+bias)");
   if (out == DType::F32) launch_bf16_layout<float>(g, ta, tb, s);
   else launch_bf16_layout<bf16>(g, ta, tb, s);
 }

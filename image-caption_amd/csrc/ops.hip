@@ -526,6 +526,78 @@ void cross_entropy_rows(const float* logits, const int32_t* tgt, int M, int V, i
   CAPGEN_HIP(hipGetLastError());
 }
 
+// Second half of the fused classifier + cross entropy (GemmArgs::ce_stats): the classifier GEMM
+// left e = exp(v - mx_c) in bf16 and {mx_c, s_c} per 16-column slab c of each row.  One
+// workgroup per row: lse = M + log sum_c s_c exp(mx_c - M), loss_row = lse - v[tgt], and the
+// row is rewritten in place as softmax - onehot = e * exp(mx_c - lse) - onehot.  Every load of the
+// row (stats + the thread's slabs) is issued up front: one memory round trip.
+template <int SPT>
+__global__ void __launch_bounds__(256) ce_finish_kernel(const float2* __restrict__ stats, int64_t ld,
+                                                        const float* __restrict__ tlogit,
+                                                        const int32_t* __restrict__ tgt, int V, int pad,
+                                                        float* __restrict__ loss_row, bf16* __restrict__ dl) {
+  __shared__ float sh[4];
+  typedef __attribute__((ext_vector_type(4))) __bf16 b4;
+  const int m = blockIdx.x, nsl = (V + 15) / 16;
+  bf16* row = dl + (int64_t)m * V;
+  const int y = tgt[m];
+  if (y == pad) {
+    for (int c = threadIdx.x * 4; c < V; c += 256 * 4) *reinterpret_cast<b4*>(row + c) = b4{0, 0, 0, 0};
+    if (threadIdx.x == 0) loss_row[m] = 0.f;
+    return;
+  }
+  float2 st[SPT];
+  b4 e[SPT][4];
+#pragma unroll
+  for (int u = 0; u < SPT; ++u) {
+    const int c = threadIdx.x + 256 * u;
+    st[u] = c < nsl ? stats[(int64_t)m * ld + c] : float2{-INFINITY, 0.f};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int col = c * 16 + q * 4;
+      e[u][q] = c < nsl && col < V ? *reinterpret_cast<const b4*>(row + col) : b4{0, 0, 0, 0};
+    }
+  }
+  const float tl = threadIdx.x == 0 ? tlogit[m] : 0.f;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < SPT; ++u) mx = fmaxf(mx, st[u].x);
+  mx = block_max(mx, sh);
+  float se = 0.f;
+#pragma unroll
+  for (int u = 0; u < SPT; ++u) se += st[u].y == 0.f ? 0.f : st[u].y * expf(st[u].x - mx);
+  se = block_sum(se, sh);
+  const float lse = mx + logf(se);
+#pragma unroll
+  for (int u = 0; u < SPT; ++u) {
+    const int c = threadIdx.x + 256 * u;
+    if (c >= nsl) continue;
+    const float f = expf(st[u].x - lse);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int col = c * 16 + q * 4;
+      if (col >= V) continue;
+      float o[4] = {(float)e[u][q][0] * f, (float)e[u][q][1] * f, (float)e[u][q][2] * f, (float)e[u][q][3] * f};
+      if (y >= col && y < col + 4) o[y - col] -= 1.f;
+      *reinterpret_cast<b4*>(row + col) = b4{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+    }
+  }
+  if (threadIdx.x == 0) loss_row[m] = lse - tl;
+}
+void ce_finish(const float2* stats, int64_t ld, const float* tlogit, const int32_t* tgt, int M, int V, int pad,
+               float* loss_row, bf16* dl, hipStream_t s) {
+  if (M <= 0) return;
+  require(V % 4 == 0 && ld >= (V + 15) / 16, "ce_finish: V must be a multiple of 4");
+  const int spt = ((V + 15) / 16 + 255) / 256;
+  if (spt <= 1) ce_finish_kernel<1><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl);
+  else if (spt <= 2) ce_finish_kernel<2><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl);
+  else if (spt <= 3) ce_finish_kernel<3><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl);
+  else if (spt <= 4) ce_finish_kernel<4><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl);
+  else if (spt <= 8) ce_finish_kernel<8><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl);
+  else throw Error("ce_finish: V > 32768");
+  CAPGEN_HIP(hipGetLastError());
+}
+
 // CE mean over the (global) non-pad count and the FocalLoss transform (model.py:73-76,
 // loss.py:20-28, gamma = 2, applied to the already-averaged CE).  ce_in != null: the mean CE is
 // given (the data-parallel path all-reduces the per-rank partial sums first); partial: only
