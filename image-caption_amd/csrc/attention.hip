@@ -12,6 +12,8 @@
 //
 // Semantics (modules.py:16-27, 67-92): s = (q / temperature) . k^T; masked_fill(-inf);
 // softmax; dropout; o = p . v.  Backward recomputes the dropout mask from the counter RNG.
+#include <cstdlib>
+
 #include "attention.h"
 
 namespace capgen {
@@ -284,6 +286,66 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnGeom g, T* __restr
   o[(int64_t)b * g.o_bs + h * 64 + lane] = from_f<T>(acc);
 }
 
+// Cross-attention decode step when several rows read one image's K/V (beam search: rows
+// j*kv_bmod + i all attend over image i; no kv_row indirection, no causal / key-id mask): one
+// workgroup per (image, head) stages V in LDS once, each of its 4 waves holds K (lane = key) in
+// registers (L1 hits after the first wave) and runs queries w, w + 4, ... of the image's
+// G = B / kv_bmod.  Each query's arithmetic is attn_decode_kernel's, in the same order
+// (bit-identical results); the image's K/V leave L2 once per (image, head), not G times.
+template <typename T>
+__global__ void __launch_bounds__(256) attn_decode_group_kernel(AttnGeom g, int G, T* __restrict__ o,
+                                                                float* __restrict__ probs) {
+  __shared__ float qsh[4][64];
+  __shared__ T vsh[64 * 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nimg = g.kv_bmod, i = blockIdx.x / g.H, h = blockIdx.x % g.H;
+  const T* kb = reinterpret_cast<const T*>(g.k) + (int64_t)i * g.k_bs + h * 64;
+  const T* vb = reinterpret_cast<const T*>(g.v) + (int64_t)i * g.v_bs + h * 64;
+  constexpr int V = 16 / sizeof(T);
+  typedef typename Vec16<T>::type VT;
+  for (int c = threadIdx.x; c < g.Lk * (64 / V); c += 256) {
+    const int jj = c / (64 / V), d0 = (c % (64 / V)) * V;
+    *reinterpret_cast<VT*>(&vsh[jj * 64 + d0]) = *reinterpret_cast<const VT*>(vb + (int64_t)jj * g.v_ld + d0);
+  }
+  const int j = lane;
+  float kx[64];
+  if (j < g.Lk) {
+#pragma unroll
+    for (int d0 = 0; d0 < 64; d0 += V) {
+      float t[V];
+      load_f<T, V>(kb + (int64_t)j * g.k_ld + d0, t);
+#pragma unroll
+      for (int e = 0; e < V; ++e) kx[d0 + e] = t[e];
+    }
+  }
+  __syncthreads();
+  for (int qi = wv; qi < G; qi += 4) {
+    const int b = qi * nimg + i;
+    qsh[wv][lane] = to_f(reinterpret_cast<const T*>(g.q)[(int64_t)b * g.q_bs + h * 64 + lane]) / g.temperature;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float s = -INFINITY;
+    if (j < g.Lk && !key_masked(g, b, 0, j)) {
+      float acc = 0.f;
+#pragma unroll
+      for (int d = 0; d < 64; ++d) acc = fmaf(qsh[wv][d], kx[d], acc);
+      s = acc;
+    }
+    const float mx = wave_max(s);
+    const float e = j < g.Lk ? expf(s - mx) : 0.f;
+    const float sum = wave_sum(e);
+    const float p = e / sum;
+    if (probs && j < g.Lk) probs[(((int64_t)b * g.H + h)) * g.Lk + j] = p;
+    float acc = 0.f;
+    for (int jj = 0; jj < g.Lk; ++jj) acc = fmaf(__shfl(p, jj, 64), to_f(vsh[jj * 64 + lane]), acc);
+    o[(int64_t)b * g.o_bs + h * 64 + lane] = from_f<T>(acc);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // this query's qsh reads before the next write
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
 __global__ void head_mean_kernel(const float* __restrict__ probs, int B, int H, int Lq, int Lk, int row,
                                  float* __restrict__ out) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -292,6 +354,15 @@ __global__ void head_mean_kernel(const float* __restrict__ probs, int B, int H, 
   float acc = 0.f;
   for (int h = 0; h < H; ++h) acc += probs[(((int64_t)b * H + h) * Lq + row) * Lk + j];
   out[c] = acc / (float)H;
+}
+
+// CAPGEN_DECODE_GROUP=0: every decode row reads its image's K/V itself (A/B knob)
+static bool group_decode_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("CAPGEN_DECODE_GROUP");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 static void check_geom(const AttnGeom& g) {
@@ -322,6 +393,14 @@ void attention_fwd(const AttnGeom& g, void* o, float* probs, DType t, hipStream_
   check_geom(g);
   if (g.Lq == 1 && g.dk == 64 && g.drop.seed_ptr == nullptr && g.q_ld % 8 == 0 && g.k_ld % 8 == 0 &&
       ((g.q_bs | g.k_bs) % 8) == 0) {  // KV-cached decode step
+    const int G = g.kv_bmod > 0 ? g.B / g.kv_bmod : 1;
+    if (G >= 2 && G <= 16 && g.B % g.kv_bmod == 0 && !g.kv_row && !g.causal && !g.key_ids && group_decode_on()) {
+      const int gblocks = g.kv_bmod * g.H;  // one workgroup per (image, head): its rows' K/V read once
+      if (t == DType::F32) attn_decode_group_kernel<float><<<gblocks, 256, 0, s>>>(g, G, (float*)o, probs);
+      else attn_decode_group_kernel<bf16><<<gblocks, 256, 0, s>>>(g, G, (bf16*)o, probs);
+      CAPGEN_HIP(hipGetLastError());
+      return;
+    }
     const int blocks = (g.B * g.H + 3) / 4;
     if (t == DType::F32) attn_decode_kernel<float><<<blocks, 256, 0, s>>>(g, (float*)o, probs);
     else attn_decode_kernel<bf16><<<blocks, 256, 0, s>>>(g, (bf16*)o, probs);

@@ -822,6 +822,25 @@ static void launch_bf16_tiles(const GemmArgs& g, hipStream_t s) {
     }();
     if (dwv) c = Choice{dwv % 100, std::max(1, dwv / 100)};
   }
+  // experiment knob: CAPGEN_GEMM_FORCE="M,N,K,ta,tb,v[;...]" pins one shape's choice (variant v +
+  // 100 * split-K), e.g. to A/B a critical-path GEMM in the step rather than alone
+  static const std::map<TuneKey, int> forced = [] {
+    std::map<TuneKey, int> m;
+    if (const char* e = std::getenv("CAPGEN_GEMM_FORCE")) {
+      int M, N, K, ta, tb, v, n = 0;
+      for (const char* p = e; *p;) {
+        if (std::sscanf(p, "%d,%d,%d,%d,%d,%d%n", &M, &N, &K, &ta, &tb, &v, &n) != 6) break;
+        m[TuneKey{M, N, K, ta, tb, 2}] = v, m[TuneKey{M, N, K, ta, tb, 4}] = v;
+        p += n;
+        if (*p == ';') ++p;
+      }
+    }
+    return m;
+  }();
+  if (c.variant == 0 && !forced.empty()) {
+    auto it = forced.find(TuneKey{g.M, g.N, g.K, TA, TB, (int)sizeof(TO)});
+    if (it != forced.end()) c = Choice{it->second % 100, std::max(1, it->second / 100)};
+  }
   if (c.splitk > 1) ensure_ws(s, splitk_bytes(g, c.splitk));
   if (c.variant == 0) {
     c.variant = heuristic_variant(g);
@@ -913,6 +932,11 @@ static void launch_group(const GemmArgs* ps, int n, hipStream_t s) {
   std::vector<int> key{TA, TB, (int)sizeof(TO)};
   for (int i = 0; i < n; ++i) key.insert(key.end(), {ps[i].M, ps[i].N, ps[i].K});
   int v = g_variant % 100;
+  static const int forced = [] {  // experiment knob: every grouped launch on one variant
+    const char* e = std::getenv("CAPGEN_DWG_VARIANT");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (v == 0 && forced) v = forced;
   if (v == 0) {
     std::lock_guard<std::mutex> lk(g_tune_mu);
     auto it = g_group_tuned.find(key);
