@@ -158,3 +158,41 @@ if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "matrix3":
     # decoder-side shapes (M = 64 x 19 = 1216 rows)
     matrix([(1216, 512, 2048, 0, 0, 0), (1216, 512, 2048, 0, 1, 0), (1216, 2048, 512, 0, 1, 0),
             (1216, 512, 512, 0, 0, 0), (1216, 512, 512, 0, 1, 0)], sks=(1, 2, 3, 4))
+
+
+def cold(shapes, choices):
+    """Event-timed eager launches, each after a 64 MB scrub write (the autotuner's cold-L2 clock)."""
+    scrub = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
+    for (M, N, K, ta, tb, f32) in shapes:
+        A = torch.randn((K, M) if ta else (M, K), device="cuda", dtype=torch.bfloat16)
+        Bm = torch.randn((K, N) if tb else (N, K), device="cuda", dtype=torch.bfloat16)
+        Cc = torch.empty(M, N, device="cuda", dtype=torch.float32 if f32 else torch.bfloat16)
+        res = []
+        for ch in choices:
+            _lib.check(lib.capgen_debug_gemm_variant(ch))
+            s = torch.cuda.current_stream()
+            call = lambda: _lib.check(lib.capgen_debug_gemm(
+                M, N, K, C.c_void_p(A.data_ptr()), M if ta else K, ta, C.c_void_p(Bm.data_ptr()), N if tb else K,
+                tb, C.c_void_p(Cc.data_ptr()), N, 1, 0 if f32 else 1, None, 1.0, 0, 0, C.c_void_p(s.cuda_stream)))
+            call()
+            tot = 0.0
+            for r in range(10):
+                scrub.fill_(r)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                call()
+                e1.record()
+                e1.synchronize()
+                tot += e0.elapsed_time(e1) * 1e3
+            res.append((tot / 10, ch))
+        _lib.check(lib.capgen_debug_gemm_variant(0))
+        print(f"M={M} N={N} K={K} ta={ta} tb={tb}: " + ", ".join(f"v{c % 100}x{max(1, c // 100)} {us:.2f}"
+                                                           for us, c in sorted(res)), flush=True)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "cold":
+    # the LN-producing shapes (N = d = 512) under the tuner's cold-L2 clock
+    # (profiles/r02_fullrow_probe.txt also ranked a since-removed 32x512 full-row variant here)
+    cold([(2304, 512, 512, 0, 0, 0), (1216, 512, 512, 0, 0, 0), (2304, 512, 2048, 0, 0, 0),
+          (1216, 512, 2048, 0, 0, 0), (2304, 512, 2048, 0, 1, 0), (1216, 512, 512, 0, 1, 0)],
+         [7, 21, 6, 12, 17, 207, 221, 307])

@@ -29,3 +29,4 @@ timeout -s KILL 90 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --ke
   -d "$out/pmc_mfma" -o run -- python3 bench.py --steps 6 --warmup 3 --no-cpu-baseline --no-host-batches > "$out/pmc_mfma.log" 2>&1 \
   || { tail -20 "$out/pmc_mfma.log"; exit 1; }
 python tools/pmc_mfma.py "$out/pmc_mfma" "$out/pmc_mfma.json" | head -6
+python tools/class_table.py "$out" > "$out/class_table.txt" && cat "$out/class_table.txt"
