@@ -89,6 +89,7 @@ struct Acts {
   float2* ce_stats;  // fused classifier + CE (bf16): {max, sum exp} per row and 16-column slab
   float* ce_tl;      // its target logits
   float *loss_row, *grad_scale, *loss, *loss_ce;
+  void* gEnc;     // encoder-chain residual gradient while decoder block 0 finishes on es2 (overlap_dec0)
   float* gEnc32;  // f32 partial sum of the encoder-output gradient over decoder blocks Ld-1 .. 1
   // SCST (rl.hip): per-row sample / lse / logp[sample] / entropy, per-image entropy, scalars
   int32_t* rl_sample;
@@ -415,6 +416,7 @@ struct capgen_engine {
     p.take(a.loss, 4);
     p.take(a.loss_ce, 4);
     p.take(a.gEnc32, (size_t)Me * d);
+    T_(a.gEnc, Me * d);
     p.take(a.rl_sample, Md);
     p.take(a.rl_lse, Md);
     p.take(a.rl_logp, Md);
@@ -886,6 +888,14 @@ struct capgen_engine {
   // partial sum -- instead of one K = 2 d Ld GEMM.  Measured slower (3.45 vs 3.41 ms/step at
   // C2: the side GEMMs queue behind the weight-gradient groups on es2 and the critical stream
   // waits for them), so off unless CAPGEN_SPLIT_ENC_GRAD=1 (experiment knob)
+  // Decoder block 0's self-attention half (and the decoder-embedding branch) on es2, concurrent
+  // with the encoder chain: once block 0's cross-attention backward has produced its K/V
+  // gradient, the encoder-output gradient (all blocks' gKV . Wkv_all) is complete, and nothing
+  // the encoder backward reads depends on the rest of block 0 (CAPGEN_OVERLAP_DEC0=0: serial)
+  bool overlap_dec0 = [] {
+    const char* e = std::getenv("CAPGEN_OVERLAP_DEC0");
+    return !(e && e[0] == '0');
+  }();
   bool split_enc_grad = [] {
     const char* e = std::getenv("CAPGEN_SPLIT_ENC_GRAD");
     return e && e[0] == '1';
@@ -1038,6 +1048,7 @@ struct capgen_engine {
   }
 
   // step_params: bucketed all-reduce + Adam (see bucket()); otherwise gradients only
+  bool dec0_on_side = false;  // backward(): decoder block 0 was issued on es2 (overlap_dec0)
   void backward(hipStream_t s, bool step_params = false) {
     bstep = step_params;
     require(fB > 0, "backward: call forward first");
@@ -1118,8 +1129,12 @@ struct capgen_engine {
                                                 d, a.gEnc32, d, Me, 2 * dd, d, l != L.Ld - 1),
                                         l == 1});
       }
-      dw_side(gb.gQc, dd, A.D1, dd, w.Wq_c, dd, Md, dd, dd, nullptr, s);
-      linear_dx(gb.gQc, dd, w.Wq_c, dd, gO, dd, Md, dd, dd, 1, nullptr, nullptr, s);  // gO = grad wrt D1
+      // block 0: the rest of the block runs on es2 (ov), the encoder chain starts on s below
+      const bool ov = l == 0 && overlap_dec0 && es2 != s;
+      const hipStream_t hs = ov ? es2 : s;
+      if (ov) flush(s);  // es2 waits for block 0's cross-attention backward; queued dW issued
+      dw_side(gb.gQc, dd, A.D1, dd, w.Wq_c, dd, Md, dd, dd, nullptr, hs);
+      linear_dx(gb.gQc, dd, w.Wq_c, dd, gO, dd, Md, dd, dd, 1, nullptr, nullptr, hs);  // gO = grad wrt D1
       AttnGeom g;
       g.B = B, g.H = Hd, g.Lq = Lq, g.Lk = Lq, g.dk = dkd;
       g.q = A.qkv, g.q_ld = 3 * dd, g.q_bs = (int64_t)Lq * 3 * dd;
@@ -1129,17 +1144,20 @@ struct capgen_engine {
       g.key_ids = a.ids, g.kid_bs = Lq, g.pad_idx = cfg.pad_idx, g.causal = 1;  // as in forward
       g.temperature = std::sqrt((float)dkd);
       g.drop = mk_drop(pa, site(1, l, 3), on);
-      mha_out_bwd(Md, dd, lself, A.atts, w.Wo_s, gb.gATT1, s);  // gR = grad wrt D_l (residual part)
-      attb(g, A.Ps, gb.gATT1, gb.gQKV, at(gb.gQKV, dd), at(gb.gQKV, 2 * dd), act, s);
-      dw_side(gb.gQKV, 3 * dd, a.D[l], dd, w.Wqkv, dd, Md, 3 * dd, dd, nullptr, s);
-      linear_dx(gb.gQKV, 3 * dd, w.Wqkv, dd, gR, dd, Md, 3 * dd, dd, 1, nullptr, nullptr, s);
+      mha_out_bwd(Md, dd, lself, A.atts, w.Wo_s, gb.gATT1, hs);  // gR = grad wrt D_l (residual part)
+      attb(g, A.Ps, gb.gATT1, gb.gQKV, at(gb.gQKV, dd), at(gb.gQKV, 2 * dd), act, hs);
+      dw_side(gb.gQKV, 3 * dd, a.D[l], dd, w.Wqkv, dd, Md, 3 * dd, dd, nullptr, hs);
+      linear_dx(gb.gQKV, 3 * dd, w.Wqkv, dd, gR, dd, Md, 3 * dd, dd, 1, nullptr, nullptr, hs);
       if (l % bucket_blocks == 0)  // blocks l .. l + bucket_blocks - 1 (contiguous in the arena)
-        bucket(w.Wqkv, dec_end(std::min(l + bucket_blocks - 1, L.Ld - 1)) - w.Wqkv, s);
+        bucket(w.Wqkv, dec_end(std::min(l + bucket_blocks - 1, L.Ld - 1)) - w.Wqkv, hs);
+      if (ov) dec0_on_side = true;
       std::swap(gO, gR);  // gO = grad wrt D_l
     }
     // cross K/V of all decoder blocks -> encoder output (the encoder chain starts here; the
     // Wkv_all weight gradient is queued after the dX GEMM below, which reads Wkv_all)
-    void* eO = gO == a.gOut ? a.gRes : a.gOut;  // the buffer gO is not using
+    // the buffer gO is not using -- or, with block 0 finishing on es2 (both in use there), gEnc
+    void* eO = dec0_on_side ? a.gEnc : gO == a.gOut ? a.gRes : a.gOut;
+    dec0_on_side = false;
     // decoder embedding: LN(E.Wel^T + PE) (model.py:432-436) -- off the critical path
     {
       const LnBwd lb = dec_emb_lb(gO);
