@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcapgen.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 F32, BF16 = 0, 1
 
@@ -83,6 +83,9 @@ _SIGS = {
     "capgen_dp_unique_id": (C.c_int, [C.c_char_p]),
     "capgen_dp_init": (C.c_int, [_P, C.c_char_p, C.c_int, C.c_int]),
     "capgen_dp_set_global_count": (C.c_int, [_P, C.c_float]),
+    "capgen_dp_sync_adam_state": (C.c_int, [_P]),
+    "capgen_dp_buckets": (C.c_int, [_P, _P, _P, C.c_int, _P]),
+    "capgen_dp_debug_shard": (C.c_int, [_P, C.c_int, C.c_int]),
     "capgen_scst_rewards": (C.c_int, [_P, C.c_int64, _P, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                       C.c_int64, C.c_double, C.c_double, _P]),
 }

@@ -98,6 +98,18 @@ class Engine:
         torch.cuda.current_stream(self.device).synchronize()
         _lib.check(self.lib.capgen_set_grads(self.h, a.ctypes.data_as(C.c_void_p), self.arena_elems))
 
+    def params_arena(self) -> np.ndarray:
+        """The whole f32 parameter arena as a host copy."""
+        torch.cuda.current_stream(self.device).synchronize()
+        return self._arena_to_host(self.lib.capgen_get_params)
+
+    def set_params_arena(self, arena: np.ndarray):
+        """Overwrite the whole f32 parameter arena (and the bf16 shadow) from host memory."""
+        a = np.ascontiguousarray(arena, dtype=np.float32)
+        assert a.size == self.arena_elems
+        torch.cuda.current_stream(self.device).synchronize()
+        _lib.check(self.lib.capgen_set_params(self.h, a.ctypes.data_as(C.c_void_p), self.arena_elems))
+
     def grads_arena(self) -> np.ndarray:
         """The whole f32 gradient arena as a host copy."""
         torch.cuda.current_stream(self.device).synchronize()
@@ -266,3 +278,21 @@ class Engine:
 
     def dp_set_global_count(self, count: float):
         _lib.check(self.lib.capgen_dp_set_global_count(self.h, float(count)))
+
+    def dp_sync_adam_state(self):
+        """Collective (every rank): all-gather the sharded Adam moments (see capgen.h)."""
+        _lib.check(self.lib.capgen_dp_sync_adam_state(self.h))
+
+    def dp_buckets(self):
+        """The last train step's gradient buckets as [(offset, count)] over the parameter arena."""
+        cap = 256
+        offs = np.zeros(cap, np.int64)
+        cnts = np.zeros(cap, np.int64)
+        n = C.c_int(0)
+        _lib.check(self.lib.capgen_dp_buckets(self.h, offs.ctypes.data_as(C.c_void_p),
+                                              cnts.ctypes.data_as(C.c_void_p), cap, C.byref(n)))
+        return [(int(offs[i]), int(cnts[i])) for i in range(n.value)]
+
+    def dp_debug_shard(self, rank: int, world: int):
+        """Test hook: update as rank `rank` of `world` would under the sharded update, no collectives."""
+        _lib.check(self.lib.capgen_dp_debug_shard(self.h, int(rank), int(world)))

@@ -227,6 +227,26 @@ struct capgen_engine {
   float* count_host = nullptr;  // pinned: global count override
   hipEvent_t ev_count = nullptr;  // recorded after the copy of count_host (host writes wait for it)
   bool count_override = false;
+  // sharded update (ZeRO-1, SURVEY §8(e) "later"): with world > 1 each bucket's gradients are
+  // reduce-scattered, each rank runs Adam on its 1/world chunk only (its chunk of the moments is
+  // the only one it keeps current), the updated f32 chunk is all-gathered in place and the bf16
+  // shadow of the bucket re-cast locally.  Same bytes over xGMI as the all-reduce (RS + AG), 1/world
+  // of the 1.67 GB Adam stream.  CAPGEN_ZERO=0: all-reduce + full Adam on every rank;
+  // CAPGEN_ZERO=2: the sharded code path even at world 1 (RCCL test hook).
+  int zero_mode = [] {
+    const char* e = std::getenv("CAPGEN_ZERO");
+    return e ? std::atoi(e) : 1;
+  }();
+  int zemu_rank = 0, zemu_world = 1;  // capgen_dp_debug_shard: shard as rank r of w, no collectives
+  std::vector<std::array<int64_t, 2>> zbuckets;  // this step's bucket ranges, in issue order
+  bool zbuckets_checked = false;
+  int zworld() const {
+    if (zemu_world > 1) return zemu_world;
+    if (!comm || zero_mode == 0) return 1;
+    return world > 1 || zero_mode == 2 ? world : 1;
+  }
+  int zrank() const { return zemu_world > 1 ? zemu_rank : rank; }
+  bool zsharded() const { return zemu_world > 1 || (comm && (world > 1 ? zero_mode != 0 : zero_mode == 2)); }
 
   // ------------------------------------------------------------------------------------
   const void* W(int64_t off) const {
@@ -978,8 +998,35 @@ struct capgen_engine {
   }
   // the bucket's all-reduce (DP) + Adam on the bucket stream (its producers already waited for)
   void bucket_update(int64_t off, int64_t n) {
+    zbuckets.push_back({off, n});
+    const int zw = zworld();
+    if (zsharded() && n % (4 * zw) == 0) {  // sharded update (ZeRO-1); buckets are 64-element aligned
+      const int64_t c = n / zw, o = off + (int64_t)zrank() * c;
+      // in place: rank r's chunk of the summed gradients lands at grads + o
+      if (comm) NCCL_CHECK(ncclReduceScatter(grads + off, grads + o, (size_t)c, ncclFloat, ncclSum, comm, ec));
+      const int64_t ns = shadow ? std::max<int64_t>(0, std::min(n, L.n_dense - off)) : 0;
+      adam_update(params + o, grads + o, am + o, av + o, (size_t)c, cfg.beta1, cfg.beta2, cfg.eps, adam_scal, nullptr, 0,
+                  ec);
+      // in place: every rank's updated chunk -> params + off (sendbuff = recvbuff + rank * c)
+      if (comm) NCCL_CHECK(ncclAllGather(params + o, params + off, (size_t)c, ncclFloat, comm, ec));
+      if (ns > 0) to_bf16(params + off, shadow + off, (size_t)ns, ec);
+      return;
+    }
     if (comm) NCCL_CHECK(ncclAllReduce(grads + off, grads + off, (size_t)n, ncclFloat, ncclSum, comm, ec));
     adam_range(off, n, ec);
+  }
+  // once: the step's buckets cover the arena exactly (each element updated by exactly one bucket)
+  void check_buckets() {
+    if (zbuckets_checked) return;
+    auto v = zbuckets;
+    std::sort(v.begin(), v.end());
+    int64_t end = 0;
+    for (auto& b : v) {
+      require(b[0] == end && b[1] > 0, "internal: gradient buckets do not tile the parameter arena");
+      end = b[0] + b[1];
+    }
+    require(end == L.total, "internal: gradient buckets do not cover the parameter arena");
+    zbuckets_checked = true;
   }
   int64_t enc_end(int l) const { return l + 1 < L.Le ? L.enc[l + 1].Wqkv : L.Wel; }
   int64_t dec_end(int l) const { return l + 1 < L.Ld ? L.dec[l + 1].Wqkv : L.Wkv_all; }
@@ -1059,7 +1106,10 @@ struct capgen_engine {
     // accumulated-gradient region (embedding table) and the striped LN/bias partials start at 0
     CAPGEN_HIP(hipMemsetAsync(grads + L.n_dense, 0, (L.enc_lng - L.n_dense) * sizeof(float), s));
     CAPGEN_HIP(hipMemsetAsync(gstripe, 0, (size_t)NSTRIPE * n_small * sizeof(float), s));
-    if (bstep) adam_prepare(step, cfg.lr, cfg.beta1, cfg.beta2, adam_scal, s);
+    if (bstep) {
+      adam_prepare(step, cfg.lr, cfg.beta1, cfg.beta2, adam_scal, s);
+      zbuckets.clear();
+    }
 
     RowMask dmask{};
     dmask.ids = a.ids, dmask.pad_idx = cfg.pad_idx;
@@ -1225,6 +1275,7 @@ struct capgen_engine {
     if (bstep) {
       dep(ec, s, ev_cj);
       bstep = false;
+      check_buckets();
     }
   }
 
@@ -2111,6 +2162,42 @@ int capgen_dp_init(capgen_t* h, const char id[128], int rank, int world) {
     NCCL_CHECK(ncclBroadcast(h->params, h->params, (size_t)h->L.total, ncclFloat, 0, h->comm, h->es));
     h->refresh_shadow(h->es);
     CAPGEN_HIP(hipStreamSynchronize(h->es));
+  });
+}
+
+int capgen_dp_sync_adam_state(capgen_t* h) {
+  return guarded([&] {
+    set_device(h);
+    CAPGEN_HIP(hipStreamSynchronize(h->es));
+    CAPGEN_HIP(hipStreamSynchronize(h->ec));
+    const int zw = h->zworld();
+    if (!h->comm || zw <= 1 || !h->zsharded()) return;
+    for (auto& b : h->zbuckets) {
+      if (b[1] % (4 * zw)) continue;  // updated by all-reduce + full Adam: already replicated
+      const int64_t c = b[1] / zw, o = b[0] + (int64_t)h->zrank() * c;
+      NCCL_CHECK(ncclAllGather(h->am + o, h->am + b[0], (size_t)c, ncclFloat, h->comm, h->es));
+      NCCL_CHECK(ncclAllGather(h->av + o, h->av + b[0], (size_t)c, ncclFloat, h->comm, h->es));
+    }
+    CAPGEN_HIP(hipStreamSynchronize(h->es));
+  });
+}
+
+int capgen_dp_buckets(capgen_t* h, int64_t* offs, int64_t* counts, int cap, int* n) {
+  return guarded([&] {
+    require(h != nullptr && n != nullptr, "dp_buckets: null argument");
+    require((int)h->zbuckets.size() <= cap, "dp_buckets: capacity too small");
+    for (size_t i = 0; i < h->zbuckets.size(); ++i) offs[i] = h->zbuckets[i][0], counts[i] = h->zbuckets[i][1];
+    *n = (int)h->zbuckets.size();
+  });
+}
+
+int capgen_dp_debug_shard(capgen_t* h, int rank, int world) {
+  return guarded([&] {
+    require(h != nullptr, "null engine handle");
+    require(world <= 1 || (rank >= 0 && rank < world), "dp_debug_shard: bad rank/world");
+    require(world <= 1 || !h->comm, "dp_debug_shard: not with a communicator");
+    h->zemu_rank = world > 1 ? rank : 0;
+    h->zemu_world = world > 1 ? world : 1;
   });
 }
 

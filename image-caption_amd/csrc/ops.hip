@@ -682,8 +682,24 @@ __global__ void to_bf16_kernel(const float* __restrict__ src, bf16* __restrict__
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
     dst[i] = (bf16)src[i];
 }
+// 4 elements per lane: one dwordx4 load, one 8-byte store (the sharded update's shadow re-cast)
+__global__ void to_bf16x4_kernel(const float4* __restrict__ src, bf16* __restrict__ dst, size_t n4) {
+  typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    const float4 x = src[i];
+    bf16x4 o = {(bf16)x.x, (bf16)x.y, (bf16)x.z, (bf16)x.w};
+    *reinterpret_cast<bf16x4*>(dst + 4 * i) = o;
+  }
+}
 void to_bf16(const float* src, bf16* dst, size_t n, hipStream_t s) {
   if (!n) return;
+  if (n % 4 == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 7) == 0) {
+    const size_t n4 = n / 4;
+    int grid = (int)std::min<size_t>((n4 + 255) / 256, 2048);
+    to_bf16x4_kernel<<<grid, 256, 0, s>>>((const float4*)src, dst, n4);
+    CAPGEN_HIP(hipGetLastError());
+    return;
+  }
   int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
   to_bf16_kernel<<<grid, 256, 0, s>>>(src, dst, n);
   CAPGEN_HIP(hipGetLastError());

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define CAPGEN_ABI_VERSION 4
+#define CAPGEN_ABI_VERSION 5
 
 typedef struct capgen_engine capgen_t;
 
@@ -216,6 +216,21 @@ int capgen_dp_init(capgen_t* h, const char id[128], int rank, int world);
  * loss output is the GLOBAL mean (Focal) loss: the per-rank partial CE sums are all-reduced before
  * the FocalLoss transform and the gradient scale (model.py:73-76, loss.py:20-28). */
 int capgen_dp_set_global_count(capgen_t* h, float count);
+
+/* Sharded parameter update (ZeRO-1; replaces the per-bucket all-reduce + full Adam that
+ * torch.optim.Adam.step over DDP-averaged gradients would be, core/models.py:111-113,124-125).
+ * With world > 1 (default; CAPGEN_ZERO=0 disables) every gradient bucket is reduce-scattered,
+ * each rank runs Adam on its 1/world chunk, and the updated f32 chunk is all-gathered in place.
+ * Parameters stay replicated on every rank after each step; the Adam moments are current only
+ * in this rank's chunks -- capgen_dp_sync_adam_state (collective, every rank) all-gathers them
+ * before capgen_get_adam_state is used for a checkpoint.
+ * capgen_dp_buckets: the last train step's bucket ranges [off, off + count) over the parameter
+ * arena, in issue order (rank r owns [off + r*count/world, off + (r+1)*count/world) of each).
+ * capgen_dp_debug_shard (test hook): without any collective, update as rank `rank` of `world`
+ * would (Adam on this rank's chunks only); world <= 1 turns it off. */
+int capgen_dp_sync_adam_state(capgen_t* h);
+int capgen_dp_buckets(capgen_t* h, int64_t* offs, int64_t* counts, int cap, int* n);
+int capgen_dp_debug_shard(capgen_t* h, int rank, int world);
 
 #ifdef __cplusplus
 }

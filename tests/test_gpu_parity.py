@@ -199,6 +199,81 @@ def test_dp_exact_global_mean_two_half_batch_engines_fp32():
     _params_close(a, full, 1e-6)
 
 
+@pytest.mark.parametrize("world,dtype", [(2, "fp32"), (8, "fp32"), (4, "bf16")])
+def test_sharded_update_chunks_equal_full_adam(world, dtype):
+    """Sharded update (ZeRO-1, engine.hip bucket_update): rank r of `world` runs Adam only on
+    chunk r of every gradient bucket.  `world` engines emulating the ranks (capgen_dp_debug_shard:
+    no collectives, each sees the full batch = the reduce-scattered gradient) each update exactly
+    their chunks, the chunks tile the arena, and the assembled parameters (what the in-place
+    all-gather leaves on every rank) equal one engine's full bucketed Adam -- for two steps, so
+    each rank's moment chunks carry over (torch.optim.Adam semantics, models.py:111-113)."""
+    cfg, seed, z = load_fixture("c2s")
+    f, p, c = _inputs(z)
+    ref = _engine(cfg, seed, dtype)
+    ranks = [_engine(cfg, seed, dtype) for _ in range(world)]
+    for r, e in enumerate(ranks):
+        e.set_training(False)
+        e.dp_debug_shard(r, world)
+    ref.set_training(False)
+    before = ref.params_arena()
+    tol = 1e-6 if dtype == "fp32" else 1e-5
+    for step in range(2):
+        lr_ = ref.train_step(f, p, c).item()
+        for e in ranks:
+            assert abs(e.train_step(f, p, c).item() - lr_) <= 1e-6 * abs(lr_)
+        want = ref.params_arena()
+        buckets = ref.dp_buckets()
+        assert buckets == ranks[0].dp_buckets()
+        got = np.full_like(want, np.nan)
+        owned = np.zeros(want.size, np.int32)
+        for r, e in enumerate(ranks):
+            pr = e.params_arena()
+            mine = np.zeros(want.size, bool)
+            for off, n in buckets:
+                assert n % (4 * world) == 0, (off, n)
+                ch = n // world
+                mine[off + r * ch: off + (r + 1) * ch] = True
+            owned += mine
+            got[mine] = pr[mine]
+            # chunks this rank does not own are left as they were (the all-gather overwrites them)
+            np.testing.assert_array_equal(pr[~mine], before[~mine])
+        assert (owned == 1).all(), "the ranks' chunks must tile the parameter arena exactly once"
+        scale = np.abs(want).max()
+        np.testing.assert_allclose(got, want, atol=tol * scale, rtol=0)
+        for e in ranks:  # the all-gather, emulated
+            e.set_params_arena(got)
+        before = got
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_sharded_update_world1_rccl_fp32(monkeypatch, graph):
+    """The sharded update's RCCL calls (in-place reduce-scatter of each bucket, Adam on the
+    chunk, in-place all-gather, local bf16 re-cast) at world size 1 (CAPGEN_ZERO=2 forces the
+    path) equal the single-process step."""
+    from capgen.engine import Engine
+    monkeypatch.setenv("CAPGEN_ZERO", "2")
+    cfg, seed, z = load_fixture("c1")
+    f, p, c = _inputs(z)
+    a = _engine(cfg, seed)
+    monkeypatch.delenv("CAPGEN_ZERO")
+    b = _engine(cfg, seed)
+    for e in (a, b):
+        e.set_training(False)
+        e.set_graph(graph)
+    a.dp_init(Engine.dp_unique_id(), 0, 1)
+    for _ in range(3):
+        la = a.train_step(f, p, c).clone()
+        lb = b.train_step(f, p, c).clone()
+        torch.cuda.synchronize()
+        assert abs(la.item() - lb.item()) < 1e-5 * abs(lb.item())
+    _params_close(a, b, 1e-6)
+    a.dp_sync_adam_state()
+    sa, sb = a.adam_state(), b.adam_state()
+    assert sa[0] == sb[0] == 3
+    for k in sa[1]:
+        torch.testing.assert_close(sa[1][k], sb[1][k], atol=1e-6, rtol=0, msg=k)
+
+
 @pytest.mark.parametrize("tag", ["c1", "c1_focal"])
 def test_dp_world1_loss_path_equals_single_process_fp32(tag):
     """The DP loss path (per-rank partial CE, 4-byte all-reduce, then CE mean / FocalLoss and the
