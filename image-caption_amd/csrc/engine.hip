@@ -98,6 +98,7 @@ struct Acts {
   // every other gradient buffer is per block, so the weight-gradient GEMMs that read them can
   // run later on the side stream without a write-after-read hazard.
   void *tmp, *gOut, *gRes, *gKV, *gE, *gAe, *gAd;
+  void* tmpf;  // the decoder front's GEMM -> LayerNorm scratch (runs on es2 beside the encoder)
   struct GradBufs {
     void *gAf, *gH, *gA1, *gATT1, *gQKV, *gA2, *gATT2, *gQc;
   };
@@ -172,6 +173,7 @@ struct capgen_engine {
   hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_b1 = nullptr, ev_b2 = nullptr, ev_cj = nullptr;
   hipEvent_t ev_part = nullptr;  // es2: the encoder-output gradient partials are summed
+  hipEvent_t ev_ff = nullptr, ev_fj = nullptr;  // forward: decoder front forked to / joined from es2
   float *params = nullptr, *grads = nullptr, *am = nullptr, *av = nullptr;
   bf16* shadow = nullptr;
   float* pe = nullptr;  // [max_length-1, dd] f32 sinusoid table
@@ -402,6 +404,7 @@ struct capgen_engine {
     p.take(a.count, 4);
     T_(a.E, Md * L_().dwe);
     T_(a.dv0, Md * dd);
+    T_(a.tmpf, Md * dd);
     p.take(a.dm0, Md);
     p.take(a.dr0, Md);
     a.D.resize(L_().Ld + 1);
@@ -709,6 +712,47 @@ struct capgen_engine {
         NCCL_CHECK(ncclAllReduce(a.count, a.count, 1, ncclFloat, ncclSum, comm, s));
     }
 
+    // ---- decoder front (model.py:432-436 and block 0's self-attention half + cross query,
+    // modules.py:185-197): depends on the captions only, so with overlap_front it runs on es2
+    // beside the whole encoder and joins before block 0's cross attention
+    RowMask dmask{};
+    dmask.ids = a.ids, dmask.pad_idx = cfg.pad_idx;
+    const bool front = overlap_front && es2 != s;
+    auto dec_embed = [&](void* tmp, hipStream_t fs) {
+      embedding_gather(P(L.emb), a.ids, 1, Md, L.dwe, a.E, act, fs);
+      LnFwd ln;
+      ln.M = Md, ln.d = dd, ln.a = tmp, ln.pe = pe, ln.pe_L = Lq, ln.gamma = P(L.dec_lng), ln.beta = P(L.dec_lnb);
+      ln.y = a.D[0], ln.v_save = a.dv0, ln.mean = a.dm0, ln.rstd = a.dr0;
+      linear_ln(a.E, L.dwe, L.Wel, L.dwe, Md, dd, L.dwe, ln, fs);
+    };
+    // self attention: key-pad(ids) OR causal (model.py:421-430), then the cross-attention query
+    auto dec_self_half = [&](int l, void* tmp, hipStream_t fs) {
+      const auto& w = L.dec[l];
+      auto& A = a.dec[l];
+      linear(a.D[l], dd, w.Wqkv, dd, A.qkv, 3 * dd, act, Md, 3 * dd, dd, nullptr, 0, fs);
+      AttnGeom g;
+      g.B = B, g.H = Hd, g.Lq = Lq, g.Lk = Lq, g.dk = dkd;
+      g.q = A.qkv, g.q_ld = 3 * dd, g.q_bs = (int64_t)Lq * 3 * dd;
+      g.k = at(A.qkv, dd), g.k_ld = 3 * dd, g.k_bs = (int64_t)Lq * 3 * dd;
+      g.v = at(A.qkv, 2 * dd), g.v_ld = 3 * dd, g.v_bs = (int64_t)Lq * 3 * dd;
+      g.o_ld = dd, g.o_bs = (int64_t)Lq * dd;
+      g.key_ids = a.ids, g.kid_bs = Lq, g.pad_idx = cfg.pad_idx, g.causal = 1;
+      g.temperature = std::sqrt((float)dkd);
+      g.drop = mk_drop(pa, site(1, l, 3), drop_on);
+      attf(g, A.atts, keep_probs(g) ? A.Ps : nullptr, act, fs);
+      LnFwd l1;
+      l1.M = Md, l1.d = dd, l1.a = tmp, l1.drop = mk_drop(p, site(1, l, 4), drop_on), l1.res = a.D[l];
+      l1.gamma = P(w.lsg), l1.beta = P(w.lsb), l1.y = A.D1, l1.v_save = A.vs, l1.mean = A.ms, l1.rstd = A.rs;
+      linear_ln(A.atts, dd, w.Wo_s, dd, Md, dd, dd, l1, fs);
+      linear(A.D1, dd, w.Wq_c, dd, A.qc, dd, act, Md, dd, dd, nullptr, 0, fs);
+    };
+    if (front) {
+      dep(s, es2, ev_ff);
+      dec_embed(a.tmpf, es2);
+      dec_self_half(0, a.tmpf, es2);
+      CAPGEN_HIP(hipEventRecord(ev_fj, es2));
+    }
+
     // ---- encoder (model.py:294-332) ----
     if (L.has_img) {
       image_objects_fwd(B, N, drop_on, s);
@@ -724,37 +768,14 @@ struct capgen_engine {
     linear(a.X[L.Le], d, L.Wkv_all, d, a.KV, (int64_t)L.Ld * 2 * dd, act, Me, L.Ld * 2 * dd, d, nullptr, 0, s);
 
     // ---- decoder (model.py:419-459) ----
-    embedding_gather(P(L.emb), a.ids, 1, Md, L.dwe, a.E, act, s);
-    {
-      LnFwd ln;
-      ln.M = Md, ln.d = dd, ln.a = a.tmp, ln.pe = pe, ln.pe_L = Lq, ln.gamma = P(L.dec_lng), ln.beta = P(L.dec_lnb);
-      ln.y = a.D[0], ln.v_save = a.dv0, ln.mean = a.dm0, ln.rstd = a.dr0;
-      linear_ln(a.E, L.dwe, L.Wel, L.dwe, Md, dd, L.dwe, ln, s);
-    }
-    RowMask dmask{};
-    dmask.ids = a.ids, dmask.pad_idx = cfg.pad_idx;
+    if (front) CAPGEN_HIP(hipStreamWaitEvent(s, ev_fj, 0));
+    else dec_embed(a.tmp, s);
     const int64_t kvld = (int64_t)L.Ld * 2 * dd;
     for (int l = 0; l < L.Ld; ++l) {
       const auto& w = L.dec[l];
       auto& A = a.dec[l];
-      // self attention: key-pad(ids) OR causal (model.py:421-430)
-      linear(a.D[l], dd, w.Wqkv, dd, A.qkv, 3 * dd, act, Md, 3 * dd, dd, nullptr, 0, s);
-      AttnGeom g;
-      g.B = B, g.H = Hd, g.Lq = Lq, g.Lk = Lq, g.dk = dkd;
-      g.q = A.qkv, g.q_ld = 3 * dd, g.q_bs = (int64_t)Lq * 3 * dd;
-      g.k = at(A.qkv, dd), g.k_ld = 3 * dd, g.k_bs = (int64_t)Lq * 3 * dd;
-      g.v = at(A.qkv, 2 * dd), g.v_ld = 3 * dd, g.v_bs = (int64_t)Lq * 3 * dd;
-      g.o_ld = dd, g.o_bs = (int64_t)Lq * dd;
-      g.key_ids = a.ids, g.kid_bs = Lq, g.pad_idx = cfg.pad_idx, g.causal = 1;
-      g.temperature = std::sqrt((float)dkd);
-      g.drop = mk_drop(pa, site(1, l, 3), drop_on);
-      attf(g, A.atts, keep_probs(g) ? A.Ps : nullptr, act, s);
-      LnFwd l1;
-      l1.M = Md, l1.d = dd, l1.a = a.tmp, l1.drop = mk_drop(p, site(1, l, 4), drop_on), l1.res = a.D[l];
-      l1.gamma = P(w.lsg), l1.beta = P(w.lsb), l1.y = A.D1, l1.v_save = A.vs, l1.mean = A.ms, l1.rstd = A.rs;
-      linear_ln(A.atts, dd, w.Wo_s, dd, Md, dd, dd, l1, s);
+      if (!(front && l == 0)) dec_self_half(l, a.tmp, s);
       // cross attention over the encoder output, context mask = region key-pad (model.py:82)
-      linear(A.D1, dd, w.Wq_c, dd, A.qc, dd, act, Md, dd, dd, nullptr, 0, s);
       AttnGeom c;
       c.B = B, c.H = Hd, c.Lq = Lq, c.Lk = N, c.dk = dkd;
       c.q = A.qc, c.q_ld = dd, c.q_bs = (int64_t)Lq * dd;
@@ -912,6 +933,10 @@ struct capgen_engine {
   // with the encoder chain: once block 0's cross-attention backward has produced its K/V
   // gradient, the encoder-output gradient (all blocks' gKV . Wkv_all) is complete, and nothing
   // the encoder backward reads depends on the rest of block 0 (CAPGEN_OVERLAP_DEC0=0: serial)
+  bool overlap_front = [] {  // CAPGEN_OVERLAP_FRONT=0: the decoder front runs after the encoder
+    const char* e = std::getenv("CAPGEN_OVERLAP_FRONT");
+    return !(e && e[0] == '0');
+  }();
   bool overlap_dec0 = [] {
     const char* e = std::getenv("CAPGEN_OVERLAP_DEC0");
     return !(e && e[0] == '0');
@@ -1704,7 +1729,7 @@ struct capgen_engine {
     if (ev_out) (void)hipEventDestroy(ev_out);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
-    for (hipEvent_t e : {ev_b1, ev_b2, ev_cj, ev_count, ev_part})
+    for (hipEvent_t e : {ev_b1, ev_b2, ev_cj, ev_count, ev_part, ev_ff, ev_fj})
       if (e) (void)hipEventDestroy(e);
     if (ec && ec != es && ec != es2) (void)hipStreamSynchronize(ec), (void)hipStreamDestroy(ec);
     if (es2 && es2 != es) (void)hipStreamSynchronize(es2), (void)hipStreamDestroy(es2);
@@ -1803,7 +1828,7 @@ int capgen_create(const capgen_config* cfg, int device, capgen_t** out) {
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
     if (nstreams >= 3) CAPGEN_HIP(hipStreamCreateWithFlags(&h->ec, hipStreamNonBlocking));
     else h->ec = h->es2;
-    for (hipEvent_t* e : {&h->ev_b1, &h->ev_b2, &h->ev_cj, &h->ev_part})
+    for (hipEvent_t* e : {&h->ev_b1, &h->ev_b2, &h->ev_cj, &h->ev_part, &h->ev_ff, &h->ev_fj})
       CAPGEN_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_count, hipEventDisableTiming));

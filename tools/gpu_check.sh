@@ -20,7 +20,7 @@ for st in "${steps[@]}"; do
     prof)
       rm -rf gpurun_out/prof
       timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
-        python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/prof.log 2>&1 \
+        python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-host-batches > gpurun_out/prof.log 2>&1 \
         || { tail -20 gpurun_out/prof.log; exit 1; }
       f=$(find gpurun_out/prof -name 'run_kernel_trace.csv' | head -1)
       mv "$(dirname "$f")"/run_* gpurun_out/prof/ 2>/dev/null
