@@ -174,6 +174,7 @@ struct capgen_engine {
   hipEvent_t ev_b1 = nullptr, ev_b2 = nullptr, ev_cj = nullptr;
   hipEvent_t ev_part = nullptr;  // es2: the encoder-output gradient partials are summed
   hipEvent_t ev_ff = nullptr, ev_fj = nullptr;  // forward: decoder front forked to / joined from es2
+  hipEvent_t ev_kv = nullptr;  // forward (kv_split): decoder blocks 1.. cross K/V done on es2
   float *params = nullptr, *grads = nullptr, *am = nullptr, *av = nullptr;
   bf16* shadow = nullptr;
   float* pe = nullptr;  // [max_length-1, dd] f32 sinusoid table
@@ -764,8 +765,17 @@ struct capgen_engine {
     }
     for (int l = 0; l < L.Le; ++l)
       enc_layer_fwd(L.enc[l], a.enc[l], a.X[l], a.X[l + 1], B, N, cfg.encode_mask ? a.valid : nullptr, l, drop_on, s);
-    // cross-attention K/V of every decoder block in one GEMM over the encoder output
-    linear(a.X[L.Le], d, L.Wkv_all, d, a.KV, (int64_t)L.Ld * 2 * dd, act, Me, L.Ld * 2 * dd, d, nullptr, 0, s);
+    // cross-attention K/V of every decoder block in one GEMM over the encoder output; with
+    // kv_split block 0's slice first, the other blocks' on es2 beside decoder block 0
+    const bool kvs = kv_split && front && L.Ld > 1;
+    const int nkv0 = kvs ? 2 * dd : L.Ld * 2 * dd;
+    linear(a.X[L.Le], d, L.Wkv_all, d, a.KV, (int64_t)L.Ld * 2 * dd, act, Me, nkv0, d, nullptr, 0, s);
+    if (kvs) {
+      dep(s, es2, ev_ff);
+      linear(a.X[L.Le], d, L.Wkv_all + (int64_t)nkv0 * d, d, at(a.KV, nkv0), (int64_t)L.Ld * 2 * dd, act, Me,
+             (L.Ld - 1) * 2 * dd, d, nullptr, 0, es2);
+      CAPGEN_HIP(hipEventRecord(ev_kv, es2));
+    }
 
     // ---- decoder (model.py:419-459) ----
     if (front) CAPGEN_HIP(hipStreamWaitEvent(s, ev_fj, 0));
@@ -775,6 +785,7 @@ struct capgen_engine {
       const auto& w = L.dec[l];
       auto& A = a.dec[l];
       if (!(front && l == 0)) dec_self_half(l, a.tmp, s);
+      if (kvs && l == 1) CAPGEN_HIP(hipStreamWaitEvent(s, ev_kv, 0));
       // cross attention over the encoder output, context mask = region key-pad (model.py:82)
       AttnGeom c;
       c.B = B, c.H = Hd, c.Lq = Lq, c.Lk = N, c.dk = dkd;
@@ -936,6 +947,10 @@ struct capgen_engine {
   bool overlap_front = [] {  // CAPGEN_OVERLAP_FRONT=0: the decoder front runs after the encoder
     const char* e = std::getenv("CAPGEN_OVERLAP_FRONT");
     return !(e && e[0] == '0');
+  }();
+  bool kv_split = [] {  // CAPGEN_KV_SPLIT=1: decoder blocks 1.. cross K/V GEMM on es2 (experiment)
+    const char* e = std::getenv("CAPGEN_KV_SPLIT");
+    return e && e[0] == '1';
   }();
   bool overlap_dec0 = [] {
     const char* e = std::getenv("CAPGEN_OVERLAP_DEC0");
@@ -1729,7 +1744,7 @@ struct capgen_engine {
     if (ev_out) (void)hipEventDestroy(ev_out);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
-    for (hipEvent_t e : {ev_b1, ev_b2, ev_cj, ev_count, ev_part, ev_ff, ev_fj})
+    for (hipEvent_t e : {ev_b1, ev_b2, ev_cj, ev_count, ev_part, ev_ff, ev_fj, ev_kv})
       if (e) (void)hipEventDestroy(e);
     if (ec && ec != es && ec != es2) (void)hipStreamSynchronize(ec), (void)hipStreamDestroy(ec);
     if (es2 && es2 != es) (void)hipStreamSynchronize(es2), (void)hipStreamDestroy(es2);
@@ -1828,7 +1843,7 @@ int capgen_create(const capgen_config* cfg, int device, capgen_t** out) {
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
     if (nstreams >= 3) CAPGEN_HIP(hipStreamCreateWithFlags(&h->ec, hipStreamNonBlocking));
     else h->ec = h->es2;
-    for (hipEvent_t* e : {&h->ev_b1, &h->ev_b2, &h->ev_cj, &h->ev_part, &h->ev_ff, &h->ev_fj})
+    for (hipEvent_t* e : {&h->ev_b1, &h->ev_b2, &h->ev_cj, &h->ev_part, &h->ev_ff, &h->ev_fj, &h->ev_kv})
       CAPGEN_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_count, hipEventDisableTiming));

@@ -672,9 +672,10 @@ void adam_update(float* p, const float* g, float* m, float* v, size_t n, float b
   require(n % 4 == 0 && n_shadow % 4 == 0, "adam: arena size must be a multiple of 4");
   if (skip_mask() & 32) return;
   size_t n4 = n / 4;
-  static const int cap = [] {  // experiment knob: Adam workgroups (grid-stride; default 8 per CU)
+  static const int cap = [] {  // Adam workgroups (grid-stride): one per CU leaves the other wave slots to the
+    // critical stream (A/B over 4 runs each: 3.046 vs 3.070 ms/step with 8 per CU; CAPGEN_ADAM_GRID)
     const char* e = std::getenv("CAPGEN_ADAM_GRID");
-    return e ? std::max(1, std::atoi(e)) : 256 * 8;
+    return e ? std::max(1, std::atoi(e)) : 256;
   }();
   int grid = (int)std::min<size_t>((n4 + 255) / 256, (size_t)cap);
   adam_kernel<<<grid, 256, 0, s>>>((float4*)p, (const float4*)g, (float4*)m, (float4*)v, n4, b1, b2, eps, scal,
