@@ -14,6 +14,8 @@
 // softmax; dropout; o = p . v.  Backward recomputes the dropout mask from the counter RNG.
 #include <cstdlib>
 
+#include <type_traits>
+
 #include "attention.h"
 
 namespace capgen {
@@ -228,122 +230,278 @@ __global__ void __launch_bounds__(AT_THREADS) attn_bwd_kernel(AttnGeom g, const 
   }
 }
 
+static bool group_decode_on();
 // Single-query attention (KV-cached decode step, model.py:101-200 with a cache): one wave64 per
-// (row, head), lane = key for the scores / softmax and lane = head dim for P.V.  Every sum runs in
-// the same order as attn_fwd_kernel (q / temperature first; d-sequential dots; the same wave
+// (row, head).  Every global load is issued up front -- the row-table entry of key `lane`, then
+// that key's K row (lane = key, 16-B loads) and every V row (lane = head dim, one coalesced row per
+// instruction, its base taken from the table by readlane) -- so a wave pays two memory round trips
+// (round 1 staged V through LDS behind a barrier and loaded K after it: four).  Arithmetic as
+// attn_fwd_kernel's, in the same order (q / temperature first; d-sequential dots; the same wave
 // butterflies; j-sequential P.V), so f32 results are bit-identical to it.  No dropout (decode).
-template <typename T>
+template <typename T, int LKM>
 __global__ void __launch_bounds__(256) attn_decode_kernel(AttnGeom g, T* __restrict__ o, float* __restrict__ probs) {
   __shared__ float qsh[4][64];
-  __shared__ T vsh[4][64 * 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int w = blockIdx.x * 4 + wv;
-  const bool live = w < g.B * g.H;
-  const int b = live ? w / g.H : 0, h = live ? w % g.H : 0;
+  if (w >= g.B * g.H) return;  // no workgroup barrier below
+  const int b = w / g.H, h = w % g.H;
   const int bk = g.kv_bmod ? b % g.kv_bmod : b;
-  const T* q = reinterpret_cast<const T*>(g.q) + (int64_t)b * g.q_bs + h * 64;
   const T* kb = reinterpret_cast<const T*>(g.k) + (int64_t)bk * g.k_bs + h * 64;
   const T* vb = reinterpret_cast<const T*>(g.v) + (int64_t)bk * g.v_bs + h * 64;
-  // stage q / temperature (lane = dim) and the V rows (coalesced 16-B chunks) in LDS
   constexpr int V = 16 / sizeof(T);
   typedef typename Vec16<T>::type VT;
+  const int Lk = g.Lk, j = lane;
+  const int rj = g.kv_row && j < Lk ? g.kv_row[(int64_t)b * g.kv_row_ld + j] - bk : 0;
+  const bool live = j < Lk && !key_masked(g, b, 0, j);
+  const float qv = to_f(reinterpret_cast<const T*>(g.q)[(int64_t)b * g.q_bs + h * 64 + lane]) / g.temperature;
+  VT kr[64 / V];
   if (live) {
-    qsh[wv][lane] = to_f(q[lane]) / g.temperature;
-    for (int c = lane; c < g.Lk * (64 / V); c += 64) {
-      const int jj = c / (64 / V), d0 = (c % (64 / V)) * V;
-      const int64_t roff = g.kv_row ? (int64_t)(g.kv_row[(int64_t)b * g.kv_row_ld + jj] - bk) * g.v_bs : 0;
-      *reinterpret_cast<VT*>(&vsh[wv][jj * 64 + d0]) =
-          *reinterpret_cast<const VT*>(vb + roff + (int64_t)jj * g.v_ld + d0);
-    }
+    const T* kp = kb + (int64_t)rj * g.k_bs + (int64_t)j * g.k_ld;
+#pragma unroll
+    for (int c = 0; c < 64 / V; ++c) kr[c] = *reinterpret_cast<const VT*>(kp + c * V);
   }
-  __syncthreads();
-  if (!live) return;
-  const int j = lane;
-  float s = -INFINITY;
-  if (j < g.Lk && !key_masked(g, b, 0, j)) {
-    const int64_t roff = g.kv_row ? (int64_t)(g.kv_row[(int64_t)b * g.kv_row_ld + j] - bk) * g.k_bs : 0;
-    const T* kr = kb + roff + (int64_t)j * g.k_ld;
-    float kx[64];
+  T vr[LKM];
 #pragma unroll
-    for (int d0 = 0; d0 < 64; d0 += V) {
-      float t[V];
-      load_f<T, V>(kr + d0, t);
-#pragma unroll
-      for (int e = 0; e < V; ++e) kx[d0 + e] = t[e];
+  for (int jj = 0; jj < LKM; ++jj)
+    if (jj < Lk) {
+      const int r = g.kv_row ? __builtin_amdgcn_readlane(rj, jj) : 0;
+      vr[jj] = vb[(int64_t)r * g.v_bs + (int64_t)jj * g.v_ld + lane];
     }
+  qsh[wv][lane] = qv;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  float s = -INFINITY;
+  if (live) {
+    const T* kx = reinterpret_cast<const T*>(kr);
     float acc = 0.f;
 #pragma unroll
-    for (int d = 0; d < 64; ++d) acc = fmaf(qsh[wv][d], kx[d], acc);
+    for (int d = 0; d < 64; ++d) acc = fmaf(qsh[wv][d], to_f(kx[d]), acc);
     s = acc;
   }
   const float mx = wave_max(s);
-  const float e = j < g.Lk ? expf(s - mx) : 0.f;
+  const float e = j < Lk ? expf(s - mx) : 0.f;
   const float sum = wave_sum(e);
   const float p = e / sum;
-  if (probs && j < g.Lk) probs[(((int64_t)b * g.H + h)) * g.Lk + j] = p;
+  if (probs && j < Lk) probs[(((int64_t)b * g.H + h)) * Lk + j] = p;
   float acc = 0.f;
-  for (int jj = 0; jj < g.Lk; ++jj) acc = fmaf(__shfl(p, jj, 64), to_f(vsh[wv][jj * 64 + lane]), acc);
+#pragma unroll
+  for (int jj = 0; jj < LKM; ++jj)
+    if (jj < Lk) acc = fmaf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), jj)), to_f(vr[jj]), acc);
   o[(int64_t)b * g.o_bs + h * 64 + lane] = from_f<T>(acc);
 }
 
 // Cross-attention decode step when several rows read one image's K/V (beam search: rows
 // j*kv_bmod + i all attend over image i; no kv_row indirection, no causal / key-id mask): one
-// workgroup per (image, head) stages V in LDS once, each of its 4 waves holds K (lane = key) in
-// registers (L1 hits after the first wave) and runs queries w, w + 4, ... of the image's
-// G = B / kv_bmod.  Each query's arithmetic is attn_decode_kernel's, in the same order
-// (bit-identical results); the image's K/V leave L2 once per (image, head), not G times.
-template <typename T>
+// wave per (image, head) loads the image's K (lane = key) and V (lane = head dim) and the queries
+// of its G = B / kv_bmod rows once, up front, then runs the queries one after another.  Each
+// query's arithmetic is attn_decode_kernel's, in the same order (bit-identical results); the
+// image's K/V leave L2 once per (image, head), not G times.
+template <typename T, int LKM, int GM>
 __global__ void __launch_bounds__(256) attn_decode_group_kernel(AttnGeom g, int G, T* __restrict__ o,
                                                                 float* __restrict__ probs) {
   __shared__ float qsh[4][64];
-  __shared__ T vsh[64 * 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int nimg = g.kv_bmod, i = blockIdx.x / g.H, h = blockIdx.x % g.H;
+  const int nimg = g.kv_bmod, w = blockIdx.x * 4 + wv;
+  if (w >= nimg * g.H) return;  // no workgroup barrier below
+  const int i = w / g.H, h = w % g.H;
   const T* kb = reinterpret_cast<const T*>(g.k) + (int64_t)i * g.k_bs + h * 64;
   const T* vb = reinterpret_cast<const T*>(g.v) + (int64_t)i * g.v_bs + h * 64;
   constexpr int V = 16 / sizeof(T);
   typedef typename Vec16<T>::type VT;
-  for (int c = threadIdx.x; c < g.Lk * (64 / V); c += 256) {
-    const int jj = c / (64 / V), d0 = (c % (64 / V)) * V;
-    *reinterpret_cast<VT*>(&vsh[jj * 64 + d0]) = *reinterpret_cast<const VT*>(vb + (int64_t)jj * g.v_ld + d0);
-  }
-  const int j = lane;
-  float kx[64];
-  if (j < g.Lk) {
+  const int Lk = g.Lk, j = lane;
+  const bool live = j < Lk && !key_masked(g, i, 0, j);  // key mask of image i (b % kv_bmod = i)
+  VT kr[64 / V];
+  if (j < Lk) {
 #pragma unroll
-    for (int d0 = 0; d0 < 64; d0 += V) {
-      float t[V];
-      load_f<T, V>(kb + (int64_t)j * g.k_ld + d0, t);
-#pragma unroll
-      for (int e = 0; e < V; ++e) kx[d0 + e] = t[e];
-    }
+    for (int c = 0; c < 64 / V; ++c) kr[c] = *reinterpret_cast<const VT*>(kb + (int64_t)j * g.k_ld + c * V);
   }
-  __syncthreads();
-  for (int qi = wv; qi < G; qi += 4) {
+  T vr[LKM];
+#pragma unroll
+  for (int jj = 0; jj < LKM; ++jj)
+    if (jj < Lk) vr[jj] = vb[(int64_t)jj * g.v_ld + lane];
+  float qr[GM];
+#pragma unroll
+  for (int qi = 0; qi < GM; ++qi)
+    if (qi < G)
+      qr[qi] = to_f(reinterpret_cast<const T*>(g.q)[(int64_t)(qi * nimg + i) * g.q_bs + h * 64 + lane]) / g.temperature;
+  const T* kx = reinterpret_cast<const T*>(kr);
+#pragma unroll
+  for (int qi = 0; qi < GM; ++qi) {
+    if (qi >= G) continue;  // (a constant trip count: the loop unrolls and qr stays in registers)
     const int b = qi * nimg + i;
-    qsh[wv][lane] = to_f(reinterpret_cast<const T*>(g.q)[(int64_t)b * g.q_bs + h * 64 + lane]) / g.temperature;
+    qsh[wv][lane] = qr[qi];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     float s = -INFINITY;
-    if (j < g.Lk && !key_masked(g, b, 0, j)) {
+    if (live) {
       float acc = 0.f;
 #pragma unroll
-      for (int d = 0; d < 64; ++d) acc = fmaf(qsh[wv][d], kx[d], acc);
+      for (int d = 0; d < 64; ++d) acc = fmaf(qsh[wv][d], to_f(kx[d]), acc);
       s = acc;
     }
     const float mx = wave_max(s);
-    const float e = j < g.Lk ? expf(s - mx) : 0.f;
+    const float e = j < Lk ? expf(s - mx) : 0.f;
     const float sum = wave_sum(e);
     const float p = e / sum;
-    if (probs && j < g.Lk) probs[(((int64_t)b * g.H + h)) * g.Lk + j] = p;
+    if (probs && j < Lk) probs[(((int64_t)b * g.H + h)) * Lk + j] = p;
     float acc = 0.f;
-    for (int jj = 0; jj < g.Lk; ++jj) acc = fmaf(__shfl(p, jj, 64), to_f(vsh[jj * 64 + lane]), acc);
+#pragma unroll
+    for (int jj = 0; jj < LKM; ++jj)
+      if (jj < Lk) acc = fmaf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), jj)), to_f(vr[jj]), acc);
     o[(int64_t)b * g.o_bs + h * 64 + lane] = from_f<T>(acc);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // this query's qsh reads before the next write
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+}
+
+// bf16 KV-cached decode step, coalesced: lane = (key slot jr = lane / 8, 16-B chunk c = lane % 8),
+// so one load instruction brings 8 whole 128-B K (or V) rows of a head (lane = key, as in the f32
+// kernel above, touches 64 rows per instruction and is bound by the address unit).  Keys j = jr,
+// jr + 8, ... ; the 8-chunk dot, the softmax and the P.V sums reduce across lanes.  Single mode
+// (G = 1): wave = (query row, head), K/V rows through the beam row table.  Group mode (G > 1, beam
+// cross attention): workgroup = (image, head), wave wv runs queries wv, wv + 4, ... of the image's
+// G rows (K/V of the image: L1/L2 hits after the first wave).  Sums in a different order than the
+// f32 kernel (bf16 operands; the f32 path keeps the order pinned to attn_fwd_kernel).
+__device__ __forceinline__ void bf16x8_to_f(const uint4& u, float (&f)[8]) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    f[2 * e] = __uint_as_float(w[e] << 16);
+    f[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+  }
+}
+template <int NIT>
+__global__ void __launch_bounds__(256) attn_decode_bf16_kernel(AttnGeom g, int G, bf16* __restrict__ o,
+                                                               float* __restrict__ probs) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, jr = lane >> 3, c = lane & 7;
+  const bool group = G > 1;
+  int b0, h, bk, qfirst, qstep;
+  if (group) {  // workgroup = (image, head); queries qi*nimg + image, qi = wv, wv + 4, ...
+    const int i = blockIdx.x / g.H;
+    h = blockIdx.x % g.H, bk = i, b0 = i, qfirst = wv, qstep = 4;
+  } else {
+    const int w = blockIdx.x * 4 + wv;
+    if (w >= g.B * g.H) return;  // no workgroup barrier in this kernel
+    b0 = w / g.H, h = w % g.H, bk = g.kv_bmod ? b0 % g.kv_bmod : b0, qfirst = 0, qstep = 1;
+  }
+  const int Lk = g.Lk;
+  const bf16* kb = reinterpret_cast<const bf16*>(g.k) + (int64_t)bk * g.k_bs + h * 64 + c * 8;
+  const bf16* vb = reinterpret_cast<const bf16*>(g.v) + (int64_t)bk * g.v_bs + h * 64 + c * 8;
+  // beam row table: lane l holds the cache row of key l (single mode only)
+  const int rl = (!group && g.kv_row && lane < Lk) ? g.kv_row[(int64_t)b0 * g.kv_row_ld + lane] - bk : 0;
+  uint4 kr[NIT], vr[NIT];
+  bool kin[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int j = jr + 8 * it;
+    kin[it] = j < Lk;
+    const int r = g.kv_row ? __shfl(rl, j < 64 ? j : 0, 64) : 0;
+    if (kin[it]) {
+      kr[it] = *reinterpret_cast<const uint4*>(kb + (int64_t)r * g.k_bs + (int64_t)j * g.k_ld);
+      vr[it] = *reinterpret_cast<const uint4*>(vb + (int64_t)r * g.v_bs + (int64_t)j * g.v_ld);
+    } else {
+      kr[it] = vr[it] = make_uint4(0, 0, 0, 0);
+    }
+  }
+  const float inv_t = 1.f / g.temperature;
+  for (int qi = qfirst; qi < G; qi += qstep) {
+    const int b = group ? qi * g.kv_bmod + b0 : b0;
+    float q[8];
+    bf16x8_to_f(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(g.q) + (int64_t)b * g.q_bs + h * 64 + c * 8),
+                q);
+    float s[NIT];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      float k[8];
+      bf16x8_to_f(kr[it], k);
+      float acc = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc = fmaf(q[e] * inv_t, k[e], acc);
+      acc += __shfl_xor(acc, 1, 64);
+      acc += __shfl_xor(acc, 2, 64);
+      acc += __shfl_xor(acc, 4, 64);
+      const int j = jr + 8 * it;
+      s[it] = kin[it] && !key_masked(g, b, 0, j) ? acc : -INFINITY;
+      mx = fmaxf(mx, s[it]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 8, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      s[it] = kin[it] ? expf(s[it] - mx) : 0.f;
+      sum += s[it];
+    }
+    sum += __shfl_xor(sum, 8, 64);
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    const float inv = 1.f / sum;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const float p = s[it] * inv;
+      if (probs && c == 0 && kin[it]) probs[((int64_t)b * g.H + h) * Lk + jr + 8 * it] = p;
+      float v[8];
+      bf16x8_to_f(vr[it], v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = fmaf(p, v[e], acc[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      acc[e] += __shfl_xor(acc[e], 8, 64);
+      acc[e] += __shfl_xor(acc[e], 16, 64);
+      acc[e] += __shfl_xor(acc[e], 32, 64);
+    }
+    if (jr == 0) {
+      uint4 u;
+      uint32_t* w = reinterpret_cast<uint32_t*>(&u);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bf16 lo = (bf16)acc[2 * e], hi = (bf16)acc[2 * e + 1];
+        w[e] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+      }
+      *reinterpret_cast<uint4*>(o + (int64_t)b * g.o_bs + h * 64 + c * 8) = u;
+    }
+  }
+}
+
+template <typename T>
+static void launch_decode(const AttnGeom& g, T* o, float* probs, hipStream_t s) {
+  const int G = g.kv_bmod > 0 ? g.B / g.kv_bmod : 1;
+  const bool grouped = G >= 2 && G <= 16 && g.B % g.kv_bmod == 0 && !g.kv_row && !g.causal && !g.key_ids &&
+                       group_decode_on();
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (((g.q_bs | g.k_bs | g.v_bs | g.k_ld | g.v_ld | g.o_bs) % 8) == 0) {
+      const int blocks = grouped ? g.kv_bmod * g.H : (g.B * g.H + 3) / 4;
+      const int Gk = grouped ? G : 1;
+      if (g.Lk <= 24) attn_decode_bf16_kernel<3><<<blocks, 256, 0, s>>>(g, Gk, o, probs);
+      else if (g.Lk <= 40) attn_decode_bf16_kernel<5><<<blocks, 256, 0, s>>>(g, Gk, o, probs);
+      else attn_decode_bf16_kernel<8><<<blocks, 256, 0, s>>>(g, Gk, o, probs);
+      CAPGEN_HIP(hipGetLastError());
+      return;
+    }
+  }
+  if (grouped) {
+    const int blocks = (g.kv_bmod * g.H + 3) / 4;  // one wave per (image, head): its rows' K/V read once
+    auto go = [&](auto lkm, auto gm) {
+      attn_decode_group_kernel<T, decltype(lkm)::value, decltype(gm)::value><<<blocks, 256, 0, s>>>(g, G, o, probs);
+    };
+    using I32 = std::integral_constant<int, 32>;
+    using I64 = std::integral_constant<int, 64>;
+    if (G <= 4) g.Lk <= 32 ? go(I32{}, std::integral_constant<int, 4>{}) : go(I64{}, std::integral_constant<int, 4>{});
+    else if (G <= 8) g.Lk <= 32 ? go(I32{}, std::integral_constant<int, 8>{}) : go(I64{}, std::integral_constant<int, 8>{});
+    else g.Lk <= 32 ? go(I32{}, std::integral_constant<int, 16>{}) : go(I64{}, std::integral_constant<int, 16>{});
+  } else {
+    const int blocks = (g.B * g.H + 3) / 4;
+    if (g.Lk <= 32) attn_decode_kernel<T, 32><<<blocks, 256, 0, s>>>(g, o, probs);
+    else attn_decode_kernel<T, 64><<<blocks, 256, 0, s>>>(g, o, probs);
+  }
+  CAPGEN_HIP(hipGetLastError());
 }
 
 __global__ void head_mean_kernel(const float* __restrict__ probs, int B, int H, int Lq, int Lk, int row,
@@ -393,18 +551,8 @@ void attention_fwd(const AttnGeom& g, void* o, float* probs, DType t, hipStream_
   check_geom(g);
   if (g.Lq == 1 && g.dk == 64 && g.drop.seed_ptr == nullptr && g.q_ld % 8 == 0 && g.k_ld % 8 == 0 &&
       ((g.q_bs | g.k_bs) % 8) == 0) {  // KV-cached decode step
-    const int G = g.kv_bmod > 0 ? g.B / g.kv_bmod : 1;
-    if (G >= 2 && G <= 16 && g.B % g.kv_bmod == 0 && !g.kv_row && !g.causal && !g.key_ids && group_decode_on()) {
-      const int gblocks = g.kv_bmod * g.H;  // one workgroup per (image, head): its rows' K/V read once
-      if (t == DType::F32) attn_decode_group_kernel<float><<<gblocks, 256, 0, s>>>(g, G, (float*)o, probs);
-      else attn_decode_group_kernel<bf16><<<gblocks, 256, 0, s>>>(g, G, (bf16*)o, probs);
-      CAPGEN_HIP(hipGetLastError());
-      return;
-    }
-    const int blocks = (g.B * g.H + 3) / 4;
-    if (t == DType::F32) attn_decode_kernel<float><<<blocks, 256, 0, s>>>(g, (float*)o, probs);
-    else attn_decode_kernel<bf16><<<blocks, 256, 0, s>>>(g, (bf16*)o, probs);
-    CAPGEN_HIP(hipGetLastError());
+    if (t == DType::F32) launch_decode<float>(g, (float*)o, probs, s);
+    else launch_decode<bf16>(g, (bf16*)o, probs, s);
     return;
   }
   if (t == DType::BF16 && !g.kv_row && attention_mfma_ok(g)) return attention_fwd_mfma(g, (bf16*)o, probs, s);

@@ -347,6 +347,20 @@ def test_beam_search_matches(tag):
     np.testing.assert_array_equal(ids.cpu().numpy(), z["beam_ids"])
 
 
+@pytest.mark.parametrize("k", [1, 3, 5])
+def test_bf16_decode_tracks_fp32(k):
+    """bf16 KV-cached decode (grouped cross-attention over an image's beam rows, beam K/V row
+    tables, fused top-k) against the fp32 engine on c2s: the same captions up to rare bf16 flips
+    (ids are pinned bit-exact to the oracle in fp32 mode, test_beam_search_matches)."""
+    cfg, seed, z = load_fixture("c2s")
+    f, p, _ = _inputs(z)
+    e32, e16 = _engine(cfg, seed), _engine(cfg, seed, dtype="bf16")
+    a = (e32.greedy(f, p)[0] if k == 1 else e32.beam(f, p, k)).cpu().numpy()
+    b = (e16.greedy(f, p)[0] if k == 1 else e16.beam(f, p, k)).cpu().numpy()
+    assert a.shape == b.shape
+    assert (a == b).mean() >= 0.8, (a, b)
+
+
 @pytest.mark.parametrize("tag", ["c1", "c2s", "c1_imgobj", "c1_movefirst"])
 def test_bf16_mode_loss_close(tag):
     cfg, seed, z = load_fixture(tag)
@@ -693,6 +707,8 @@ def test_splitk_combine_bit_reproducible_under_load():
     (2, 8, 64, 64, 64, 1, False),   # maximum length
     (2, 8, 33, 17, 64, 0, False),   # ragged tiles
     (2, 4, 9, 9, 32, 1, True),      # C1 head size (VALU kernels in both dtypes)
+    (5, 8, 1, 19, 64, 0, True),     # KV-cached decode step, self-attention length (attn_decode_kernel)
+    (5, 8, 1, 36, 64, 0, True),     # KV-cached decode step over the regions (> 32 keys)
 ])
 def test_attention_kernels_vs_torch(dtype, B, H, Lq, Lk, dk, causal, mask):
     """ScaledDotProductAttention (modules.py:16-27) forward + backward through the C ABI vs a
