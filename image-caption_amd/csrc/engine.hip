@@ -206,6 +206,36 @@ struct capgen_engine {
     return !(e && e[0] == '0');
   }();
   hipGraphExec_t fexec = nullptr;
+  // split forward graphs (CAPGEN_FWD_SPLIT=1, with the decoder front on es2): the front and the
+  // critical chain as separate LINEAR graphs on their own streams.  Under rocprofv3 the one
+  // multi-stream graph ran its front branch before the encoder (no overlap) and the split graphs
+  // overlapped, but without the profiler the single graph measured faster (4-round A/B: 3.032 vs
+  // 3.048 ms/step; front off: 3.072), so the split is off by default
+  bool fwd_split = [] {
+    const char* e = std::getenv("CAPGEN_FWD_SPLIT");
+    return e && e[0] == '1';
+  }();
+  bool cap_split = false;  // forward() is being captured in split mode: it ends/begins captures
+  hipGraph_t fg[4] = {};   // pre, front, encoder, decoder
+  hipGraphExec_t fx[4] = {};
+  void cap_cut(hipStream_t from, int idx, hipStream_t next) {  // end capture on `from` into fg[idx]
+    CAPGEN_HIP(hipStreamEndCapture(from, &fg[idx]));
+    if (next) CAPGEN_HIP(hipStreamBeginCapture(next, hipStreamCaptureModeThreadLocal));
+  }
+  void launch_fwd(hipStream_t cs) {
+    if (fexec) {
+      CAPGEN_HIP(hipGraphLaunch(fexec, cs));
+      return;
+    }
+    CAPGEN_HIP(hipGraphLaunch(fx[0], cs));
+    dep(cs, es2, ev_ff);
+    CAPGEN_HIP(hipGraphLaunch(fx[1], es2));
+    CAPGEN_HIP(hipEventRecord(ev_fj, es2));
+    CAPGEN_HIP(hipGraphLaunch(fx[2], cs));
+    CAPGEN_HIP(hipStreamWaitEvent(cs, ev_fj, 0));
+    CAPGEN_HIP(hipGraphLaunch(fx[3], cs));
+  }
+  bool have_fwd_graph() const { return fexec || fx[3]; }
   struct Key {
     const void *f, *p, *c;
     float* loss;
@@ -547,6 +577,8 @@ struct capgen_engine {
       (void)hipGraphExecDestroy(gexec);
       gexec = nullptr;
     }
+    for (auto& x : fx)
+      if (x) (void)hipGraphExecDestroy(x), x = nullptr;
     if (fexec) {
       (void)hipGraphExecDestroy(fexec);
       fexec = nullptr;
@@ -748,10 +780,12 @@ struct capgen_engine {
       linear(A.D1, dd, w.Wq_c, dd, A.qc, dd, act, Md, dd, dd, nullptr, 0, fs);
     };
     if (front) {
-      dep(s, es2, ev_ff);
+      if (cap_split) cap_cut(s, 0, es2);
+      else dep(s, es2, ev_ff);
       dec_embed(a.tmpf, es2);
       dec_self_half(0, a.tmpf, es2);
-      CAPGEN_HIP(hipEventRecord(ev_fj, es2));
+      if (cap_split) cap_cut(es2, 1, s);
+      else CAPGEN_HIP(hipEventRecord(ev_fj, es2));
     }
 
     // ---- encoder (model.py:294-332) ----
@@ -767,7 +801,7 @@ struct capgen_engine {
       enc_layer_fwd(L.enc[l], a.enc[l], a.X[l], a.X[l + 1], B, N, cfg.encode_mask ? a.valid : nullptr, l, drop_on, s);
     // cross-attention K/V of every decoder block in one GEMM over the encoder output; with
     // kv_split block 0's slice first, the other blocks' on es2 beside decoder block 0
-    const bool kvs = kv_split && front && L.Ld > 1;
+    const bool kvs = kv_split && front && !cap_split && L.Ld > 1;
     const int nkv0 = kvs ? 2 * dd : L.Ld * 2 * dd;
     linear(a.X[L.Le], d, L.Wkv_all, d, a.KV, (int64_t)L.Ld * 2 * dd, act, Me, nkv0, d, nullptr, 0, s);
     if (kvs) {
@@ -778,7 +812,8 @@ struct capgen_engine {
     }
 
     // ---- decoder (model.py:419-459) ----
-    if (front) CAPGEN_HIP(hipStreamWaitEvent(s, ev_fj, 0));
+    if (front && cap_split) cap_cut(s, 2, s);
+    else if (front) CAPGEN_HIP(hipStreamWaitEvent(s, ev_fj, 0));
     else dec_embed(a.tmp, s);
     const int64_t kvld = (int64_t)L.Ld * 2 * dd;
     for (int l = 0; l < L.Ld; ++l) {
@@ -1349,9 +1384,9 @@ struct capgen_engine {
                   hipStream_t cs) {
     ensure_acts(B, N, T);
     Key k{f, pos, caps, loss, (int)ft, B, N, T, training, in_idx, in_n_img};
-    if (direct_on && !graph_on && fwd_graph_on && !comm && fexec && fkey == k && cs != es) {
+    if (direct_on && !graph_on && fwd_graph_on && !comm && have_fwd_graph() && fkey == k && cs != es) {
       crit = cs;
-      CAPGEN_HIP(hipGraphLaunch(fexec, cs));
+      launch_fwd(cs);
       fB = B, fN = N, fT = T, fwd_drop = training;  // host state forward() would have set
       backward(cs, /*step_params=*/true);
       crit = nullptr;
@@ -1382,7 +1417,7 @@ struct capgen_engine {
       // forward replayed as one linear hipGraph (cheap to launch: ~0.1 us/node of host time vs
       // ~2.7 us per eager launch, tools/kprobe.hip); backward issued eagerly on three streams
       // (a multi-branch graph costs the same host time per node as eager issue on ROCm 7)
-      if (!(fexec && fkey == k)) {
+      if (!(have_fwd_graph() && fkey == k)) {
         drop_graph();
         if (!tuned(B, N, T)) {  // autotune every GEMM shape outside the capture
           forward(f, ft, pos, caps, B, N, T, loss, /*drop_on=*/false, es);
@@ -1391,24 +1426,39 @@ struct capgen_engine {
           tuned_shapes.push_back({B, N, T});
         }
         hipGraph_t graph = nullptr;
+        // split capture needs the decoder front on its own stream
+        cap_split = fwd_split && overlap_front && es2 != es;
         CAPGEN_HIP(hipStreamBeginCapture(es, hipStreamCaptureModeThreadLocal));
         try {
           forward(f, ft, pos, caps, B, N, T, loss, training, es);
         } catch (...) {
           (void)hipStreamEndCapture(es, &graph);
           if (graph) (void)hipGraphDestroy(graph);
+          cap_split = false;
+          for (auto& x : fg)
+            if (x) (void)hipGraphDestroy(x), x = nullptr;
           throw;
         }
         CAPGEN_HIP(hipStreamEndCapture(es, &graph));
-        CAPGEN_HIP(hipGraphInstantiate(&fexec, graph, nullptr, nullptr, 0));
-        CAPGEN_HIP(hipGraphDestroy(graph));
+        if (cap_split) {
+          fg[3] = graph;
+          for (int i = 0; i < 4; ++i) {
+            CAPGEN_HIP(hipGraphInstantiate(&fx[i], fg[i], nullptr, nullptr, 0));
+            CAPGEN_HIP(hipGraphDestroy(fg[i]));
+            fg[i] = nullptr;
+          }
+          cap_split = false;
+        } else {
+          CAPGEN_HIP(hipGraphInstantiate(&fexec, graph, nullptr, nullptr, 0));
+          CAPGEN_HIP(hipGraphDestroy(graph));
+        }
         fkey = k;
       }
       static const bool host_timing = std::getenv("CAPGEN_HOST_TIMING") != nullptr;  // diagnostic
       static double tb = 0, tl = 0;
       static int nsteps = 0;
       auto t0 = std::chrono::steady_clock::now();
-      CAPGEN_HIP(hipGraphLaunch(fexec, es));
+      launch_fwd(es);
       auto t1 = std::chrono::steady_clock::now();
       fB = B, fN = N, fT = T, fwd_drop = training;  // host state forward() would have set
       backward(es, /*step_params=*/true);
