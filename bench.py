@@ -153,6 +153,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=5)
     ap.add_argument("--no-host-batches", action="store_true", help="skip the secondary host-batch line")
+    ap.add_argument("--dp1", action="store_true",
+                    help="diagnostic: run the engine's RCCL data-parallel step at world size 1 (its collectives and, with CAPGEN_ZERO=2, the sharded update) to price the DP machinery on one GPU")
     args = ap.parse_args()
 
     from capgen import preset
@@ -174,7 +176,7 @@ def main():
     eng = Engine(cfg, dev)
     eng.load_state_dict({k: torch.from_numpy(v) for k, v in reference_init_state_dict(cfg, seed=0).items()})
     eng.set_graph(args.graph)
-    if world > 1:
+    if world > 1 or args.dp1:
         from capgen.dp import init_engine_dp
         init_engine_dp(eng, rank, world)
 

@@ -210,11 +210,15 @@ struct capgen_engine {
   // critical chain as separate LINEAR graphs on their own streams.  Under rocprofv3 the one
   // multi-stream graph ran its front branch before the encoder (no overlap) and the split graphs
   // overlapped, but without the profiler the single graph measured faster (4-round A/B: 3.032 vs
-  // 3.048 ms/step; front off: 3.072), so the split is off by default
-  bool fwd_split = [] {
+  // 3.048 ms/step; front off: 3.072).  The multi-branch graph costs the host more to launch
+  // (enqueue per step 2.52 vs 2.27 ms; linear graphs ~0.1 us per node), which matters once the
+  // step also issues the per-bucket collectives: split by default under DP with world > 1 only
+  // (CAPGEN_FWD_SPLIT=0/1 forces either)
+  int fwd_split_env = [] {
     const char* e = std::getenv("CAPGEN_FWD_SPLIT");
-    return e && e[0] == '1';
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
   }();
+  bool fwd_split() const { return fwd_split_env == 1 || (fwd_split_env < 0 && comm && world > 1); }
   bool cap_split = false;  // forward() is being captured in split mode: it ends/begins captures
   hipGraph_t fg[4] = {};   // pre, front, encoder, decoder
   hipGraphExec_t fx[4] = {};
@@ -1384,7 +1388,7 @@ struct capgen_engine {
                   hipStream_t cs) {
     ensure_acts(B, N, T);
     Key k{f, pos, caps, loss, (int)ft, B, N, T, training, in_idx, in_n_img};
-    if (direct_on && !graph_on && fwd_graph_on && !comm && have_fwd_graph() && fkey == k && cs != es) {
+    if (direct_on && !graph_on && fwd_graph_on && !count_override && have_fwd_graph() && fkey == k && cs != es) {
       crit = cs;
       launch_fwd(cs);
       fB = B, fN = N, fT = T, fwd_drop = training;  // host state forward() would have set
@@ -1413,7 +1417,10 @@ struct capgen_engine {
         }
       }
     };
-    if (!graph_on && fwd_graph_on && !comm) {
+    // under DP the forward graph holds the count and partial-CE all-reduces (RCCL ops capture);
+    // a host-set global count (capgen_dp_set_global_count) runs the forward eagerly instead --
+    // its pinned-memory copy must stay ordered against the host write
+    if (!graph_on && fwd_graph_on && !count_override) {
       // forward replayed as one linear hipGraph (cheap to launch: ~0.1 us/node of host time vs
       // ~2.7 us per eager launch, tools/kprobe.hip); backward issued eagerly on three streams
       // (a multi-branch graph costs the same host time per node as eager issue on ROCm 7)
@@ -1427,7 +1434,7 @@ struct capgen_engine {
         }
         hipGraph_t graph = nullptr;
         // split capture needs the decoder front on its own stream
-        cap_split = fwd_split && overlap_front && es2 != es;
+        cap_split = fwd_split() && overlap_front && es2 != es;
         CAPGEN_HIP(hipStreamBeginCapture(es, hipStreamCaptureModeThreadLocal));
         try {
           forward(f, ft, pos, caps, B, N, T, loss, training, es);
@@ -2296,6 +2303,7 @@ int capgen_dp_set_global_count(capgen_t* h, float count) {
     set_device(h);
     // the previous step's asynchronous copy may still be queued: it must read the old value
     CAPGEN_HIP(hipEventSynchronize(h->ev_count));
+    if (h->count_override != (count > 0.f)) h->drop_graph();  // the forward graph's count source changes
     h->count_override = count > 0.f;
     *h->count_host = count;
   });
