@@ -159,6 +159,32 @@ def test_dp_world1_rccl_train_step_fp32(graph):
     _params_close(a, b, 1e-6)
 
 
+@pytest.mark.parametrize("dp", [False, True])
+def test_split_forward_graphs_equal_eager_fp32(monkeypatch, dp):
+    """The forward as split linear graphs (pre / decoder front on es2 / encoder / decoder, events
+    between them; CAPGEN_FWD_SPLIT=1, the default under DP with world > 1) equals the eager
+    forward over three bucketed train steps, with and without the RCCL DP path (world 1)."""
+    from capgen.engine import Engine
+    cfg, seed, z = load_fixture("c2s")
+    f, p, c = _inputs(z)
+    monkeypatch.setenv("CAPGEN_FWD_SPLIT", "1")
+    a = _engine(cfg, seed)
+    monkeypatch.setenv("CAPGEN_FWD_GRAPH", "0")
+    b = _engine(cfg, seed)
+    monkeypatch.delenv("CAPGEN_FWD_SPLIT")
+    monkeypatch.delenv("CAPGEN_FWD_GRAPH")
+    for e in (a, b):
+        e.set_training(False)
+        if dp:
+            e.dp_init(Engine.dp_unique_id(), 0, 1)
+    for i in range(3):
+        la = a.train_step(f, p, c).clone()
+        lb = b.train_step(f, p, c).clone()
+        torch.cuda.synchronize()
+        assert abs(la.item() - lb.item()) <= 1e-6 * abs(lb.item()), (i, la.item(), lb.item())
+    _params_close(a, b, 1e-6)
+
+
 def test_dp_exact_global_mean_two_half_batch_engines_fp32():
     """SURVEY §8(e) exact-mean rule through the engine's DP path on one GPU: two world-1 RCCL
     engines each run HALF of the batch with capgen_dp_set_global_count(global non-pad count)
