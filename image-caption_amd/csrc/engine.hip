@@ -1038,11 +1038,18 @@ struct capgen_engine {
   }
 
   // Adam over arena ranges; ranges are 64-element aligned so the bf16 shadow slices line up
-  void adam_range(int64_t off, int64_t n, hipStream_t s) {
+  void adam_range(int64_t off, int64_t n, hipStream_t s, int grid_cap = 0) {
     const int64_t ns = shadow ? std::max<int64_t>(0, std::min(n, L.n_dense - off)) : 0;
     adam_update(params + off, grads + off, am + off, av + off, (size_t)n, cfg.beta1, cfg.beta2, cfg.eps, adam_scal,
-                ns > 0 ? shadow + off : nullptr, (size_t)ns, s);
+                ns > 0 ? shadow + off : nullptr, (size_t)ns, s, grid_cap);
   }
+  // Adam grid of the step's last buckets (embedding, encoder LN/biases), which sit between the
+  // backward's end and the next forward (CAPGEN_ADAM_TAIL_GRID; 0 = the common cap).  The whole
+  // chip for them measured slower (4-round A/B: 3.012 vs 2.982 ms/step with 2048 vs 256)
+  int tail_grid = [] {
+    const char* e = std::getenv("CAPGEN_ADAM_TAIL_GRID");
+    return e ? std::atoi(e) : 0;
+  }();
 
   // Step mode (train_step): the parameter update is bucketed.  A bucket is an arena range
   // whose gradients are final and whose weights nothing later in the backward pass reads
@@ -1076,7 +1083,7 @@ struct capgen_engine {
     bucket_update(off, n);
   }
   // the bucket's all-reduce (DP) + Adam on the bucket stream (its producers already waited for)
-  void bucket_update(int64_t off, int64_t n) {
+  void bucket_update(int64_t off, int64_t n, int grid_cap = 0) {
     zbuckets.push_back({off, n});
     const int zw = zworld();
     if (zsharded() && n % (4 * zw) == 0) {  // sharded update (ZeRO-1); buckets are 64-element aligned
@@ -1085,14 +1092,14 @@ struct capgen_engine {
       if (comm) NCCL_CHECK(ncclReduceScatter(grads + off, grads + o, (size_t)c, ncclFloat, ncclSum, comm, ec));
       const int64_t ns = shadow ? std::max<int64_t>(0, std::min(n, L.n_dense - off)) : 0;
       adam_update(params + o, grads + o, am + o, av + o, (size_t)c, cfg.beta1, cfg.beta2, cfg.eps, adam_scal, nullptr, 0,
-                  ec);
+                  ec, grid_cap);
       // in place: every rank's updated chunk -> params + off (sendbuff = recvbuff + rank * c)
       if (comm) NCCL_CHECK(ncclAllGather(params + o, params + off, (size_t)c, ncclFloat, comm, ec));
       if (ns > 0) to_bf16(params + off, shadow + off, (size_t)ns, ec);
       return;
     }
     if (comm) NCCL_CHECK(ncclAllReduce(grads + off, grads + off, (size_t)n, ncclFloat, ncclSum, comm, ec));
-    adam_range(off, n, ec);
+    adam_range(off, n, ec, grid_cap);
   }
   // once: the step's buckets cover the arena exactly (each element updated by exactly one bucket)
   void check_buckets() {
@@ -1347,8 +1354,8 @@ struct capgen_engine {
     if (bstep && L.has_img) dep(es2, ec, ev_b2);
     stripe_reduce(GS(L.enc_lng), NSTRIPE, n_small, L.dec_lng - L.enc_lng, G(L.enc_lng), 0, tail);
     if (bstep) {
-      bucket_update(0, L.enc[0].Wqkv);                   // feature/position embedding
-      bucket_update(L.enc_lng, L.dec_lng - L.enc_lng);   // encoder LN / biases
+      bucket_update(0, L.enc[0].Wqkv, tail_grid);                   // feature/position embedding
+      bucket_update(L.enc_lng, L.dec_lng - L.enc_lng, tail_grid);   // encoder LN / biases
     }
     join(s);
     if (bstep) {

@@ -668,7 +668,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float4* __restrict__ p, const
   }
 }
 void adam_update(float* p, const float* g, float* m, float* v, size_t n, float b1, float b2, float eps,
-                 const float* scal, bf16* shadow, size_t n_shadow, hipStream_t s) {
+                 const float* scal, bf16* shadow, size_t n_shadow, hipStream_t s, int grid_cap) {
   require(n % 4 == 0 && n_shadow % 4 == 0, "adam: arena size must be a multiple of 4");
   if (skip_mask() & 32) return;
   size_t n4 = n / 4;
@@ -677,7 +677,8 @@ void adam_update(float* p, const float* g, float* m, float* v, size_t n, float b
     const char* e = std::getenv("CAPGEN_ADAM_GRID");
     return e ? std::max(1, std::atoi(e)) : 256;
   }();
-  int grid = (int)std::min<size_t>((n4 + 255) / 256, (size_t)cap);
+  // grid_cap > 0: the caller's cap (an update on the step's critical path takes the whole chip)
+  int grid = (int)std::min<size_t>((n4 + 255) / 256, (size_t)(grid_cap > 0 ? grid_cap : cap));
   adam_kernel<<<grid, 256, 0, s>>>((float4*)p, (const float4*)g, (float4*)m, (float4*)v, n4, b1, b2, eps, scal,
                                    shadow, n_shadow);
   CAPGEN_HIP(hipGetLastError());
