@@ -13,6 +13,8 @@
 // buffers with register-staged global loads (issue next tile's loads before the MFMAs of
 // the current tile, write them to the other LDS buffer after).  Transposed operands are
 // transposed on the LDS write so every MFMA fragment is one 16-B ds_read (bf16).
+#include <chrono>
+#include <cstdio>
 #include "gemm.h"
 #include "ops.h"
 
@@ -210,7 +212,22 @@ static void launch_layout(const GemmArgs& g, bool ta, bool tb, hipStream_t s) {
   else launch_tiles<T, TO, true, true>(g, s);
 }
 
+static void gemm_impl(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t s);
+// CAPGEN_HOST_TIMING (diagnostic): average host time of a gemm() call, printed every 2000 calls
 void gemm(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t s) {
+  static const bool timing = std::getenv("CAPGEN_HOST_TIMING") != nullptr;
+  if (!timing) return gemm_impl(g, in, out, ta, tb, s);
+  static double tot = 0;
+  static long n = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  gemm_impl(g, in, out, ta, tb, s);
+  tot += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  if (++n % 2000 == 0) {
+    std::fprintf(stderr, "[capgen host] gemm() call: %.2f us average over 2000\n", tot / 2000);
+    tot = 0;
+  }
+}
+static void gemm_impl(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0) return;
   if ((skip_mask() & 16) && out == DType::F32) return;
   if ((skip_mask() & 64) && out == DType::BF16) return;

@@ -27,6 +27,7 @@
 //
 // Tiles BMxBNx64, 256 threads = 2x2 wave64s; blocks remapped so consecutive tiles (sharing
 // an A row-panel) land on the same XCD L2.
+#include <chrono>
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -859,10 +860,13 @@ static void launch_bf16_tiles(const GemmArgs& g, hipStream_t s) {
   }
   if (c.splitk > 1) {
     const size_t bytes = splitk_bytes(g, c.splitk);
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    CAPGEN_HIP(hipStreamIsCapturing(s, &st));
-    if (st == hipStreamCaptureStatusNone) ensure_ws(s, bytes);
-    else if (get_ws(s).bytes < bytes) c.splitk = 1;  // no allocation inside a capture
+    const Workspace w = get_ws(s);
+    if (!(w.cnt && w.bytes >= bytes)) {  // (the common case skips the capture query: host time)
+      hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+      CAPGEN_HIP(hipStreamIsCapturing(s, &st));
+      if (st == hipStreamCaptureStatusNone) ensure_ws(s, bytes);
+      else c.splitk = 1;  // no allocation inside a capture
+    }
   }
   launch_variant<TO, TA, TB>(c.variant, g, s, c.splitk);
 }
@@ -976,7 +980,22 @@ static void launch_group(const GemmArgs* ps, int n, hipStream_t s) {
   launch_group_variant<TO, TA, TB>(v, ps, n, s);
 }
 
+static void gemm_grouped_impl(const GemmArgs* ps, int n, DType out, bool ta, bool tb, hipStream_t s);
+// CAPGEN_HOST_TIMING (diagnostic): average host time of a grouped launch, printed every 500 calls
 void gemm_grouped(const GemmArgs* ps, int n, DType out, bool ta, bool tb, hipStream_t s) {
+  static const bool timing = std::getenv("CAPGEN_HOST_TIMING") != nullptr;
+  if (!timing) return gemm_grouped_impl(ps, n, out, ta, tb, s);
+  static double tot = 0;
+  static long cnt = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  gemm_grouped_impl(ps, n, out, ta, tb, s);
+  tot += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  if (++cnt % 500 == 0) {
+    std::fprintf(stderr, "[capgen host] gemm_grouped() call: %.2f us average over 500\n", tot / 500);
+    tot = 0;
+  }
+}
+static void gemm_grouped_impl(const GemmArgs* ps, int n, DType out, bool ta, bool tb, hipStream_t s) {
   require(n >= 1 && n <= kMaxGroup, "gemm_grouped: 1..kMaxGroup problems");
   int dev = 0;
   CAPGEN_HIP(hipGetDevice(&dev));
