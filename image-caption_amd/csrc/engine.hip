@@ -66,6 +66,8 @@ struct DecAct {
   float *Ps, *ms, *rs, *Pc, *mc, *rc, *mf, *rf;
 };
 
+constexpr int kLnSideSlots = 40;  // LayerNorm backward calls per backward pass with side-stream sums
+
 struct Acts {
   int B = 0, N = 0, T = 0;  // capacity
   // encoder
@@ -99,6 +101,8 @@ struct Acts {
   // run later on the side stream without a write-after-read hazard.
   void *tmp, *gOut, *gRes, *gKV, *gE, *gAe, *gAd;
   void* tmpf;  // the decoder front's GEMM -> LayerNorm scratch (runs on es2 beside the encoder)
+  std::vector<void*> lns;  // per block LayerNorm: the masked output gradient for the side-stream parameter sums
+  int64_t lns_cap = 0;     // elements per lns slot
   struct GradBufs {
     void *gAf, *gH, *gA1, *gATT1, *gQKV, *gA2, *gATT2, *gQc;
   };
@@ -343,6 +347,30 @@ struct capgen_engine {
     l.prio = prio(s);
     layernorm_bwd(l, act, s);
   }
+  // CAPGEN_LN_SUMS_SIDE=1 (experiment, off): a transformer block's LayerNorm backward on the
+  // critical stream without its parameter sums -- the kernel saves y = dy * rowmask and the
+  // dgamma / dbeta / producing-bias sums (a per-workgroup LDS reduction + striped atomics) run on
+  // es2, queued with the block's weight gradients.  Kernel level: encoder LN backward 9.98 -> 8.21
+  // us, decoder 7.93 -> 8.08 (the extra store eats the saving); step level slower (3.035 vs 3.019
+  // ms/step, 3 rounds): the 29 side kernels (6-7 us each) add to the es2 contention.
+  bool ln_sums_side = [] {
+    const char* e = std::getenv("CAPGEN_LN_SUMS_SIDE");
+    return e && e[0] == '1';
+  }();
+  std::vector<LnBwd> lns_pending;
+  int lns_next = 0;
+  void lnb_block(LnBwd l, hipStream_t s) {
+    if (!ln_sums_side || es2 == s || (!l.dgamma && !l.dbias) || lns_next >= (int)a.lns.size() ||
+        (int64_t)l.M * l.d > a.lns_cap)  // (the image block's pair rows exceed a slot: in the kernel)
+      return lnb(l, s);
+    LnBwd side = l;
+    l.y_save = a.lns[lns_next++];
+    l.dgamma = l.dbeta = l.dbias = nullptr;
+    lnb(l, s);
+    side.dy = l.y_save;
+    side.mask = RowMask{};
+    lns_pending.push_back(side);
+  }
   void attf(AttnGeom g, void* o, float* probs, DType t, hipStream_t s) const {
     g.prio = prio(s);
     attention_fwd(g, o, probs, t, s);
@@ -484,6 +512,9 @@ struct capgen_engine {
     p.take(a.rl_scal, 8);
     const int64_t dmax = std::max<int64_t>(std::max(d, dd), L_().dwe);
     T_(a.tmp, Mx * dmax);
+    a.lns.resize(kLnSideSlots);
+    for (auto& x : a.lns) T_(x, Mx * dmax);
+    a.lns_cap = (int64_t)Mx * dmax;
     T_(a.gOut, Mx * dmax);
     T_(a.gRes, Mx * dmax);
     T_(a.gKV, Me * L_().Ld * 2 * dd);
@@ -965,6 +996,8 @@ struct capgen_engine {
     dw_pending.clear();
     for (const ColJob& j : col_pending) column_sum(j.X, j.M, j.N, j.N, 1.f, nullptr, j.db, act, es2, NSTRIPE, n_small);
     col_pending.clear();
+    for (const LnBwd& l : lns_pending) layernorm_param_sums(l, act, es2);
+    lns_pending.clear();
     for (const SideGemm& j : nn_pending) {
       gemm(j.ga, act, DType::F32, false, true, es2);
       if (j.mark) CAPGEN_HIP(hipEventRecord(ev_part, es2));
@@ -1012,7 +1045,7 @@ struct capgen_engine {
   // X = block input, H = hidden activations.
   void ffn_bwd(int M, int d, int f, const LnBwd& lb, const void* X, const void* H, int64_t W1, int64_t b1, int64_t W2,
                void* gH, hipStream_t s) {
-    lnb(lb, s);
+    lnb_block(lb, s);
     void* gA = lb.d_a;
     dw_side(gA, d, H, f, W2, f, M, d, f, nullptr, s);
     const bool side = colsum_side && es2 != s;
@@ -1031,7 +1064,7 @@ struct capgen_engine {
       CAPGEN_HIP(hipMemcpyAsync(dbg_snap[3], lb.mean, (size_t)M * 4, hipMemcpyDeviceToDevice, s));
       CAPGEN_HIP(hipMemcpyAsync(dbg_snap[4], lb.rstd, (size_t)M * 4, hipMemcpyDeviceToDevice, s));
     }
-    lnb(lb, s);
+    lnb_block(lb, s);
     if (snap) CAPGEN_HIP(hipMemcpyAsync(dbg_snap[1], lb.d_a, (size_t)M * d * es_(), hipMemcpyDeviceToDevice, s));
     dw_side(lb.d_a, d, att, d, Wo, d, M, d, d, nullptr, s);
     linear_dx(lb.d_a, d, Wo, d, gATT, d, M, d, d, 0, nullptr, nullptr, s);
@@ -1196,6 +1229,8 @@ struct capgen_engine {
       adam_prepare(step, cfg.lr, cfg.beta1, cfg.beta2, adam_scal, s);
       zbuckets.clear();
     }
+    lns_next = 0;
+    lns_pending.clear();
 
     RowMask dmask{};
     dmask.ids = a.ids, dmask.pad_idx = cfg.pad_idx;

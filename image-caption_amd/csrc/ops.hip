@@ -89,11 +89,10 @@ __global__ void __launch_bounds__(LN_THREADS) ln_fwd_kernel(LnFwd a) {
   }
 }
 
-template <typename T, int DPL>
+template <typename T, int DPL, int R>  // R rows in flight per wave: every load of them is issued first
 __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(LnBwd a) {
   __shared__ float red[3][LN_THREADS / 64][64 * DPL];
   if (a.prio) __builtin_amdgcn_s_setprio(3);
-  constexpr int R = 2;  // rows in flight per wave: every load of both rows is issued first
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int d = a.d, c0 = lane * DPL;
   float dg[DPL], db[DPL], dz[DPL], gm[DPL];
@@ -123,10 +122,11 @@ __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(LnBwd a) {
       const int m = m0 + u * stride;
       const int64_t base = (int64_t)m * d + c0;
       const float keep = kept[u] ? 1.f : 0.f;
-      float g[DPL], xh[DPL], s1 = 0.f, s2 = 0.f;
+      float g[DPL], xh[DPL], yv[DPL], s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int e = 0; e < DPL; ++e) {
         const float y = dy[u][e] * keep;
+        yv[e] = y;
         xh[e] = (v[u][e] - mean[u]) * rstd[u];
         g[e] = y * gm[e];
         s1 += g[e];
@@ -134,6 +134,7 @@ __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(LnBwd a) {
         dg[e] = fmaf(y, xh[e], dg[e]);
         db[e] += y;
       }
+      if (a.y_save) store_f<T, DPL>(reinterpret_cast<T*>(a.y_save) + base, yv);
       const float mg = wave_sum(s1) / (float)d, mgx = wave_sum(s2) / (float)d;
       float dv[DPL];
 #pragma unroll
@@ -176,6 +177,74 @@ __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(LnBwd a) {
   }
 }
 
+// LayerNorm parameter sums on the side stream (layernorm_param_sums): the same per-workgroup
+// reduction and striped atomics as ln_bwd_kernel's tail, from y = dy * rowmask (saved by the
+// critical-path kernel), the saved LN input / statistics and d_a
+template <typename T, int DPL>
+__global__ void __launch_bounds__(LN_THREADS) ln_sums_kernel(LnBwd a) {
+  __shared__ float red[3][LN_THREADS / 64][64 * DPL];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int d = a.d, c0 = lane * DPL;
+  float dg[DPL], db[DPL], dz[DPL];
+#pragma unroll
+  for (int e = 0; e < DPL; ++e) dg[e] = db[e] = dz[e] = 0.f;
+  for (int m = blockIdx.x * (LN_THREADS / 64) + wave; m < a.M; m += gridDim.x * (LN_THREADS / 64)) {
+    const int64_t base = (int64_t)m * d + c0;
+    float y[DPL], v[DPL], z[DPL];
+    load_f<T, DPL>(reinterpret_cast<const T*>(a.dy) + base, y);
+    load_f<T, DPL>(reinterpret_cast<const T*>(a.v) + base, v);
+    if (a.dbias) load_f<T, DPL>(reinterpret_cast<const T*>(a.d_a) + base, z);
+    const float mean = a.mean[m], rstd = a.rstd[m];
+#pragma unroll
+    for (int e = 0; e < DPL; ++e) {
+      dg[e] = fmaf(y[e], (v[e] - mean) * rstd, dg[e]);
+      db[e] += y[e];
+      if (a.dbias) dz[e] += z[e];
+    }
+  }
+  const int64_t so = (int64_t)(blockIdx.x % a.stripes) * a.stripe_stride;
+#pragma unroll
+  for (int e = 0; e < DPL; ++e) {
+    red[0][wave][c0 + e] = dg[e];
+    red[1][wave][c0 + e] = db[e];
+    red[2][wave][c0 + e] = dz[e];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < d; c += LN_THREADS) {
+    float sg = 0.f, sb = 0.f, sz = 0.f;
+#pragma unroll
+    for (int w = 0; w < LN_THREADS / 64; ++w) {
+      sg += red[0][w][c];
+      sb += red[1][w][c];
+      sz += red[2][w][c];
+    }
+    if (a.dgamma) {
+      atomicAdd(a.dgamma + so + c, sg);
+      atomicAdd(a.dbeta + so + c, sb);
+    }
+    if (a.dbias) atomicAdd(a.dbias + so + c, sz);
+  }
+}
+template <typename T>
+static void ln_sums_dispatch(const LnBwd& a, hipStream_t s) {
+  dim3 grid(std::min(256, (a.M + 7) / 8));
+  switch (a.d / 64) {
+    case 1: ln_sums_kernel<T, 1><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 2: ln_sums_kernel<T, 2><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 4: ln_sums_kernel<T, 4><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 8: ln_sums_kernel<T, 8><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 16: ln_sums_kernel<T, 16><<<grid, LN_THREADS, 0, s>>>(a); break;
+    default: throw Error("layernorm: width must be 64 * {1,2,4,8,16}");
+  }
+}
+void layernorm_param_sums(const LnBwd& a, DType t, hipStream_t s) {
+  if (a.M <= 0 || (skip_mask() & 128) || (!a.dgamma && !a.dbias)) return;
+  require(a.dy && a.v && a.mean && a.rstd && (!a.dbias || a.d_a), "layernorm_param_sums: missing inputs");
+  if (t == DType::F32) ln_sums_dispatch<float>(a, s);
+  else ln_sums_dispatch<bf16>(a, s);
+  CAPGEN_HIP(hipGetLastError());
+}
+
 template <typename T>
 static void ln_fwd_dispatch(const LnFwd& a, hipStream_t s) {
   dim3 grid((a.M + 3) / 4);
@@ -195,18 +264,28 @@ void layernorm_fwd(const LnFwd& a, DType t, hipStream_t s) {
   CAPGEN_HIP(hipGetLastError());
 }
 
-template <typename T>
-static void ln_bwd_dispatch(const LnBwd& a, hipStream_t s) {
-  // two rows per wave (one loop trip at C2), <= 512 workgroups: few enough dgamma/dbeta atomics
-  dim3 grid(std::min(512, (a.M + 7) / 8));
+template <typename T, int R>
+static void ln_bwd_dispatch_r(const LnBwd& a, hipStream_t s) {
+  // R rows per wave (one loop trip at C2 for R = 2), <= 512 workgroups: few enough dgamma/dbeta atomics
+  dim3 grid(std::min(512, (a.M + 4 * R - 1) / (4 * R)));
   switch (a.d / 64) {
-    case 1: ln_bwd_kernel<T, 1><<<grid, LN_THREADS, 0, s>>>(a); break;
-    case 2: ln_bwd_kernel<T, 2><<<grid, LN_THREADS, 0, s>>>(a); break;
-    case 4: ln_bwd_kernel<T, 4><<<grid, LN_THREADS, 0, s>>>(a); break;
-    case 8: ln_bwd_kernel<T, 8><<<grid, LN_THREADS, 0, s>>>(a); break;
-    case 16: ln_bwd_kernel<T, 16><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 1: ln_bwd_kernel<T, 1, R><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 2: ln_bwd_kernel<T, 2, R><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 4: ln_bwd_kernel<T, 4, R><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 8: ln_bwd_kernel<T, 8, R><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 16: ln_bwd_kernel<T, 16, R><<<grid, LN_THREADS, 0, s>>>(a); break;
     default: throw Error("layernorm: width must be 64 * {1,2,4,8,16}");
   }
+}
+template <typename T>
+static void ln_bwd_dispatch(const LnBwd& a, hipStream_t s) {
+  static const int rows = [] {  // experiment knob: rows per wave (1, 2 or 4)
+    const char* e = std::getenv("CAPGEN_LNB_ROWS");
+    return e ? std::atoi(e) : 2;
+  }();
+  if (rows == 1) ln_bwd_dispatch_r<T, 1>(a, s);
+  else if (rows == 4) ln_bwd_dispatch_r<T, 4>(a, s);
+  else ln_bwd_dispatch_r<T, 2>(a, s);
 }
 void layernorm_bwd(const LnBwd& a_in, DType t, hipStream_t s) {
   if (a_in.M <= 0 || (skip_mask() & 4)) return;
