@@ -724,6 +724,40 @@ static bool tune_cold() {
   }();
   return on;
 }
+// CAPGEN_TUNE_BG=1 (experiment): each timed candidate runs beside a background stream kernel
+// shaped like the step's bucket Adam (one 256-thread workgroup per CU streaming 96 MB read +
+// write), so the ranking sees the contention the step's critical GEMMs run under
+__global__ void tune_bg_kernel(const float4* __restrict__ a, float4* __restrict__ b, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    float4 v = a[i];
+    v.x += 1.f;
+    b[i] = v;
+  }
+}
+static bool tune_bg() {
+  static const bool on = [] {
+    const char* e = std::getenv("CAPGEN_TUNE_BG");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+static void tune_bg_launch(hipStream_t s) {
+  static hipStream_t bg = nullptr;
+  static float4* buf = nullptr;
+  constexpr size_t kN = (48u << 20) / 16;  // 48 MB in, 48 MB out
+  if (!bg) {
+    CAPGEN_HIP(hipStreamCreateWithFlags(&bg, hipStreamNonBlocking));
+    CAPGEN_HIP(hipMalloc(&buf, 2 * kN * sizeof(float4)));
+    CAPGEN_HIP(hipMemset(buf, 0, 2 * kN * sizeof(float4)));
+    CAPGEN_HIP(hipDeviceSynchronize());
+  }
+  CAPGEN_HIP(hipStreamSynchronize(s));  // the scrub is done: background and candidate start together
+  tune_bg_kernel<<<256, 256, 0, bg>>>(buf, buf + kN, kN);
+}
+static void tune_bg_wait() {
+  CAPGEN_HIP(hipDeviceSynchronize());
+}
+
 template <typename F>
 static float tune_time(F&& launch, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   launch();  // warm-up (code, TLB)
@@ -745,10 +779,12 @@ static float tune_time(F&& launch, hipStream_t s, hipEvent_t e0, hipEvent_t e1) 
   float tot = 0.f;
   for (int r = 0; r < 3; ++r) {
     CAPGEN_HIP(hipMemsetAsync(buf, r, kScrub, s));
+    if (tune_bg()) tune_bg_launch(s);
     CAPGEN_HIP(hipEventRecord(e0, s));
     launch();
     CAPGEN_HIP(hipEventRecord(e1, s));
     CAPGEN_HIP(hipEventSynchronize(e1));
+    if (tune_bg()) tune_bg_wait();
     float ms = 0.f;
     CAPGEN_HIP(hipEventElapsedTime(&ms, e0, e1));
     tot += ms;

@@ -89,9 +89,9 @@ __global__ void __launch_bounds__(LN_THREADS) ln_fwd_kernel(LnFwd a) {
   }
 }
 
-template <typename T, int DPL, int R>  // R rows in flight per wave: every load of them is issued first
-__global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(LnBwd a) {
-  __shared__ float red[3][LN_THREADS / 64][64 * DPL];
+template <typename T, int DPL, int R, int NT = LN_THREADS>  // R rows in flight per wave: every load of them is issued first
+__global__ void __launch_bounds__(NT) ln_bwd_kernel(LnBwd a) {
+  __shared__ float red[3][NT / 64][64 * DPL];
   if (a.prio) __builtin_amdgcn_s_setprio(3);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int d = a.d, c0 = lane * DPL;
@@ -100,8 +100,8 @@ __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(LnBwd a) {
 #pragma unroll
   for (int e = 0; e < DPL; ++e) dg[e] = db[e] = dz[e] = 0.f;
   const uint64_t seed = a.drop.seed_ptr ? *a.drop.seed_ptr : 0;
-  const int stride = gridDim.x * (LN_THREADS / 64);
-  for (int m0 = blockIdx.x * (LN_THREADS / 64) + wave; m0 < a.M; m0 += R * stride) {
+  const int stride = gridDim.x * (NT / 64);
+  for (int m0 = blockIdx.x * (NT / 64) + wave; m0 < a.M; m0 += R * stride) {
     float dy[R][DPL], v[R][DPL], mean[R], rstd[R];
     bool on[R], kept[R];
 #pragma unroll
@@ -161,10 +161,10 @@ __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(LnBwd a) {
     red[2][wave][c0 + e] = dz[e];
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < d; c += LN_THREADS) {
+  for (int c = threadIdx.x; c < d; c += NT) {
     float sg = 0.f, sb = 0.f, sz = 0.f;
 #pragma unroll
-    for (int w = 0; w < LN_THREADS / 64; ++w) {
+    for (int w = 0; w < NT / 64; ++w) {
       sg += red[0][w][c];
       sb += red[1][w][c];
       sz += red[2][w][c];
@@ -264,16 +264,17 @@ void layernorm_fwd(const LnFwd& a, DType t, hipStream_t s) {
   CAPGEN_HIP(hipGetLastError());
 }
 
-template <typename T, int R>
+template <typename T, int R, int NT = LN_THREADS>
 static void ln_bwd_dispatch_r(const LnBwd& a, hipStream_t s) {
   // R rows per wave (one loop trip at C2 for R = 2), <= 512 workgroups: few enough dgamma/dbeta atomics
-  dim3 grid(std::min(512, (a.M + 4 * R - 1) / (4 * R)));
+  constexpr int W = NT / 64;
+  dim3 grid(std::min(512, (a.M + W * R - 1) / (W * R)));
   switch (a.d / 64) {
-    case 1: ln_bwd_kernel<T, 1, R><<<grid, LN_THREADS, 0, s>>>(a); break;
-    case 2: ln_bwd_kernel<T, 2, R><<<grid, LN_THREADS, 0, s>>>(a); break;
-    case 4: ln_bwd_kernel<T, 4, R><<<grid, LN_THREADS, 0, s>>>(a); break;
-    case 8: ln_bwd_kernel<T, 8, R><<<grid, LN_THREADS, 0, s>>>(a); break;
-    case 16: ln_bwd_kernel<T, 16, R><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 1: ln_bwd_kernel<T, 1, R, NT><<<grid, NT, 0, s>>>(a); break;
+    case 2: ln_bwd_kernel<T, 2, R, NT><<<grid, NT, 0, s>>>(a); break;
+    case 4: ln_bwd_kernel<T, 4, R, NT><<<grid, NT, 0, s>>>(a); break;
+    case 8: ln_bwd_kernel<T, 8, R, NT><<<grid, NT, 0, s>>>(a); break;
+    case 16: ln_bwd_kernel<T, 16, R, NT><<<grid, NT, 0, s>>>(a); break;
     default: throw Error("layernorm: width must be 64 * {1,2,4,8,16}");
   }
 }
@@ -283,7 +284,12 @@ static void ln_bwd_dispatch(const LnBwd& a, hipStream_t s) {
     const char* e = std::getenv("CAPGEN_LNB_ROWS");
     return e ? std::atoi(e) : 2;
   }();
-  if (rows == 1) ln_bwd_dispatch_r<T, 1>(a, s);
+  static const int waves = [] {  // experiment knob: waves per workgroup (4 or 8)
+    const char* e = std::getenv("CAPGEN_LNB_WAVES");
+    return e ? std::atoi(e) : 4;
+  }();
+  if (waves == 8) ln_bwd_dispatch_r<T, 2, 512>(a, s);
+  else if (rows == 1) ln_bwd_dispatch_r<T, 1>(a, s);
   else if (rows == 4) ln_bwd_dispatch_r<T, 4>(a, s);
   else ln_bwd_dispatch_r<T, 2>(a, s);
 }
