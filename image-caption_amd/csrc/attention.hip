@@ -421,14 +421,14 @@ __global__ void __launch_bounds__(256) attn_decode_bf16_kernel(AttnGeom g, int G
       float acc = 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc = fmaf(q[e] * inv_t, k[e], acc);
-      acc += __shfl_xor(acc, 1, 64);
-      acc += __shfl_xor(acc, 2, 64);
-      acc += __shfl_xor(acc, 4, 64);
+      acc += dpp_f<kDppXor1>(acc);  // the 8 chunks of key j: lanes 8 jr .. 8 jr + 7
+      acc += dpp_f<kDppXor2>(acc);
+      acc += dpp_f<kDppHalfMirror>(acc);
       const int j = jr + 8 * it;
       s[it] = kin[it] && !key_masked(g, b, 0, j) ? acc : -INFINITY;
       mx = fmaxf(mx, s[it]);
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 8, 64));
+    mx = fmaxf(mx, dpp_f<kDppRor8>(mx));
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     float sum = 0.f;
@@ -437,7 +437,7 @@ __global__ void __launch_bounds__(256) attn_decode_bf16_kernel(AttnGeom g, int G
       s[it] = kin[it] ? expf(s[it] - mx) : 0.f;
       sum += s[it];
     }
-    sum += __shfl_xor(sum, 8, 64);
+    sum += dpp_f<kDppRor8>(sum);
     sum += __shfl_xor(sum, 16, 64);
     sum += __shfl_xor(sum, 32, 64);
     const float inv = 1.f / sum;
@@ -453,7 +453,7 @@ __global__ void __launch_bounds__(256) attn_decode_bf16_kernel(AttnGeom g, int G
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      acc[e] += __shfl_xor(acc[e], 8, 64);
+      acc[e] += dpp_f<kDppRor8>(acc[e]);  // lane ^ 8: the same chunk c of the next key slot
       acc[e] += __shfl_xor(acc[e], 16, 64);
       acc[e] += __shfl_xor(acc[e], 32, 64);
     }

@@ -78,15 +78,36 @@ __device__ __forceinline__ void store_f(T* p, const float (&in)[N]) {
   }
 }
 
-// ---- wave64 reductions (DPP/permute via __shfl_xor) ----------------------------------
+// ---- wave64 reductions ----------------------------------------------------------------
+// Lane exchanges inside a 16-lane row are DPP moves (a VALU operand modifier, no LDS crossbar):
+// quad_perm swaps lanes ^1 and ^2, row_half_mirror pairs lane i with 7 - i (the other quad of the
+// same 8), row_ror:8 is exactly lane ^ 8.  Across rows (^16, ^32) they go through ds_bpermute.
+// For a commutative reduction of a value held by every lane, a mirror pairs a lane with one of
+// the complementary half as well as an xor does (every lane ends with the group total).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+constexpr int kDppXor1 = 0xB1;        // quad_perm [1,0,3,2]
+constexpr int kDppXor2 = 0x4E;        // quad_perm [2,3,0,1]
+constexpr int kDppHalfMirror = 0x141;  // lane i <-> 7 - i within 8
+constexpr int kDppRor8 = 0x128;        // lane i <-> i ^ 8 within 16
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  v += dpp_f<kDppXor1>(v);
+  v += dpp_f<kDppXor2>(v);
+  v += dpp_f<kDppHalfMirror>(v);
+  v += dpp_f<kDppRor8>(v);
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
   return v;
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  v = fmaxf(v, dpp_f<kDppXor1>(v));
+  v = fmaxf(v, dpp_f<kDppXor2>(v));
+  v = fmaxf(v, dpp_f<kDppHalfMirror>(v));
+  v = fmaxf(v, dpp_f<kDppRor8>(v));
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  v = fmaxf(v, __shfl_xor(v, 32, 64));
   return v;
 }
 
