@@ -92,6 +92,19 @@ constexpr int kDppXor1 = 0xB1;        // quad_perm [1,0,3,2]
 constexpr int kDppXor2 = 0x4E;        // quad_perm [2,3,0,1]
 constexpr int kDppHalfMirror = 0x141;  // lane i <-> 7 - i within 8
 constexpr int kDppRor8 = 0x128;        // lane i <-> i ^ 8 within 16
+// lane ^ O (or, for O = 4, the half-mirror partner): DPP inside a row, ds_bpermute across rows
+template <int O>
+__device__ __forceinline__ int lane_xchg(int v) {
+  if constexpr (O == 1) return __builtin_amdgcn_mov_dpp(v, kDppXor1, 0xf, 0xf, false);
+  else if constexpr (O == 2) return __builtin_amdgcn_mov_dpp(v, kDppXor2, 0xf, 0xf, false);
+  else if constexpr (O == 4) return __builtin_amdgcn_mov_dpp(v, kDppHalfMirror, 0xf, 0xf, false);
+  else if constexpr (O == 8) return __builtin_amdgcn_mov_dpp(v, kDppRor8, 0xf, 0xf, false);
+  else return __shfl_xor(v, O, 64);
+}
+template <int O>
+__device__ __forceinline__ float lane_xchg(float v) {
+  return __int_as_float(lane_xchg<O>(__float_as_int(v)));
+}
 __device__ __forceinline__ float wave_sum(float v) {
   v += dpp_f<kDppXor1>(v);
   v += dpp_f<kDppXor2>(v);

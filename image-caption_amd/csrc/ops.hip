@@ -825,15 +825,18 @@ __global__ void __launch_bounds__(256) argmax_softmax_kernel(const float* __rest
       bidx = c;
     }
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    float ov = __shfl_xor(best, o, 64);
-    int oi = __shfl_xor(bidx, o, 64);
+  auto merge = [&](float ov, int oi) {
     if (ov > best || (ov == best && oi < bidx)) {
       best = ov;
       bidx = oi;
     }
-  }
+  };
+  merge(lane_xchg<32>(best), lane_xchg<32>(bidx));
+  merge(lane_xchg<16>(best), lane_xchg<16>(bidx));
+  merge(lane_xchg<8>(best), lane_xchg<8>(bidx));
+  merge(lane_xchg<4>(best), lane_xchg<4>(bidx));
+  merge(lane_xchg<2>(best), lane_xchg<2>(bidx));
+  merge(lane_xchg<1>(best), lane_xchg<1>(bidx));
   if ((threadIdx.x & 63) == 0) {
     bv[threadIdx.x >> 6] = best;
     bi[threadIdx.x >> 6] = bidx;
@@ -887,14 +890,20 @@ __device__ __forceinline__ void topk_insert(float (&tv)[KM], int (&ti)[KM], floa
 }
 
 // (value, index) winner of a wave: value desc, index asc; pos rides along
+template <int O>
+__device__ __forceinline__ void best_step(float& best, int& bidx, int& bpos) {
+  const float ov = lane_xchg<O>(best);
+  const int oi = lane_xchg<O>(bidx);
+  const int op = lane_xchg<O>(bpos);
+  if (ov > best || (ov == best && oi < bidx)) best = ov, bidx = oi, bpos = op;
+}
 __device__ __forceinline__ void wave_best(float& best, int& bidx, int& bpos) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(best, o, 64);
-    const int oi = __shfl_xor(bidx, o, 64);
-    const int op = __shfl_xor(bpos, o, 64);
-    if (ov > best || (ov == best && oi < bidx)) best = ov, bidx = oi, bpos = op;
-  }
+  best_step<32>(best, bidx, bpos);
+  best_step<16>(best, bidx, bpos);
+  best_step<8>(best, bidx, bpos);
+  best_step<4>(best, bidx, bpos);
+  best_step<2>(best, bidx, bpos);
+  best_step<1>(best, bidx, bpos);
 }
 
 template <int KM, int NV>
