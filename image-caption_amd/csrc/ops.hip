@@ -800,6 +800,9 @@ void to_bf16(const float* src, bf16* dst, size_t n, hipStream_t s) {
 // logsm = 0: argmax of Softmax (Transformer, model.py:124-128); 1: of LogSoftmax
 // (PolicyNetwork, model_RL.py:72,126-127) -- the same token except where the rounding of the
 // two scores makes different near-ties
+// NV > 0: the row (V <= 256 NV) is read once into registers, every load up front (one memory
+// round trip instead of three dependent passes); the same per-thread order as the NV = 0 loops
+template <int NV>
 __global__ void __launch_bounds__(256) argmax_softmax_kernel(const float* __restrict__ logits, int V,
                                                              int64_t* ids_out, int64_t ids_ld, int col,
                                                              int32_t* next_ids, int64_t next_ld, int logsm) {
@@ -808,21 +811,51 @@ __global__ void __launch_bounds__(256) argmax_softmax_kernel(const float* __rest
   __shared__ int bi[4];
   const int b = blockIdx.x;
   const float* x = logits + (int64_t)b * V;
+  float xr[NV > 0 ? NV : 1];
   float mx = -INFINITY;
-  for (int c = threadIdx.x; c < V; c += 256) mx = fmaxf(mx, x[c]);
+  if constexpr (NV > 0) {
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int c = threadIdx.x + 256 * u;
+      xr[u] = c < V ? x[c] : -INFINITY;
+      mx = fmaxf(mx, xr[u]);
+    }
+  } else {
+    for (int c = threadIdx.x; c < V; c += 256) mx = fmaxf(mx, x[c]);
+  }
   mx = block_max(mx, sh);
   float se = 0.f;
-  for (int c = threadIdx.x; c < V; c += 256) se += expf(x[c] - mx);
+  if constexpr (NV > 0) {
+#pragma unroll
+    for (int u = 0; u < NV; ++u)
+      if (threadIdx.x + 256 * u < V) se += expf(xr[u] - mx);
+  } else {
+    for (int c = threadIdx.x; c < V; c += 256) se += expf(x[c] - mx);
+  }
   se = block_sum(se, sh);
   // argmax over the softmax probabilities, first index on ties (torch.argmax)
   float best = -INFINITY;
   int bidx = 0x7fffffff;
   const float lse = logf(se);
-  for (int c = threadIdx.x; c < V; c += 256) {
-    const float p = logsm ? (x[c] - mx) - lse : expf(x[c] - mx) / se;
-    if (p > best) {
-      best = p;
-      bidx = c;
+  if constexpr (NV > 0) {
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int c = threadIdx.x + 256 * u;
+      if (c < V) {
+        const float p = logsm ? (xr[u] - mx) - lse : expf(xr[u] - mx) / se;
+        if (p > best) {
+          best = p;
+          bidx = c;
+        }
+      }
+    }
+  } else {
+    for (int c = threadIdx.x; c < V; c += 256) {
+      const float p = logsm ? (x[c] - mx) - lse : expf(x[c] - mx) / se;
+      if (p > best) {
+        best = p;
+        bidx = c;
+      }
     }
   }
   auto merge = [&](float ov, int oi) {
@@ -856,7 +889,8 @@ __global__ void __launch_bounds__(256) argmax_softmax_kernel(const float* __rest
 }
 void argmax_softmax(const float* logits, int B, int V, int64_t* ids_out, int64_t ids_ld, int col, int32_t* next_ids,
                     int64_t next_ld, hipStream_t s, int logsm) {
-  argmax_softmax_kernel<<<B, 256, 0, s>>>(logits, V, ids_out, ids_ld, col, next_ids, next_ld, logsm);
+  if (V <= 256 * 40) argmax_softmax_kernel<40><<<B, 256, 0, s>>>(logits, V, ids_out, ids_ld, col, next_ids, next_ld, logsm);
+  else argmax_softmax_kernel<0><<<B, 256, 0, s>>>(logits, V, ids_out, ids_ld, col, next_ids, next_ld, logsm);
   CAPGEN_HIP(hipGetLastError());
 }
 
