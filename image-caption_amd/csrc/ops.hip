@@ -940,14 +940,39 @@ __device__ __forceinline__ void wave_best(float& best, int& bidx, int& bpos) {
   best_step<1>(best, bidx, bpos);
 }
 
-template <int KM, int NV>
-__global__ void __launch_bounds__(256) beam_row_topk_kernel(const float* __restrict__ logits,
+template <int W>
+__device__ __forceinline__ float blk_max(float v, float* sh) {
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float r = sh[0];
+#pragma unroll
+  for (int w = 1; w < W; ++w) r = fmaxf(r, sh[w]);
+  __syncthreads();
+  return r;
+}
+template <int W>
+__device__ __forceinline__ float blk_sum(float v, float* sh) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int w = 0; w < W; ++w) r += sh[w];
+  __syncthreads();
+  return r;
+}
+
+// NT threads per row (W = NT / 64 waves), NV values per thread in registers (V <= NT * NV)
+template <int KM, int NV, int NT = 256>
+__global__ void __launch_bounds__(NT) beam_row_topk_kernel(const float* __restrict__ logits,
                                                             const float* __restrict__ prev, int B, int V, int k,
                                                             int logsm, float* __restrict__ cand_v,
                                                             int* __restrict__ cand_i) {
-  __shared__ float sh[4];
-  __shared__ float wv[4][16];
-  __shared__ int wi[4][16];
+  constexpr int W = NT / 64;
+  __shared__ float sh[W];
+  __shared__ float wv[W][16];
+  __shared__ int wi[W][16];
   const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = r / B;
   const float* x = logits + (int64_t)r * V;
   float xr[NV > 0 ? NV : 1];
@@ -955,27 +980,27 @@ __global__ void __launch_bounds__(256) beam_row_topk_kernel(const float* __restr
   if constexpr (NV > 0) {
 #pragma unroll
     for (int u = 0; u < NV; ++u) {
-      const int c = tid + 256 * u;
+      const int c = tid + NT * u;
       xr[u] = c < V ? x[c] : -INFINITY;
       mx = fmaxf(mx, xr[u]);
     }
   } else {
-    for (int c = tid; c < V; c += 256) mx = fmaxf(mx, x[c]);
+    for (int c = tid; c < V; c += NT) mx = fmaxf(mx, x[c]);
   }
-  mx = block_max(mx, sh);
+  mx = blk_max<W>(mx, sh);
   float se = 0.f;
   if constexpr (NV > 0) {
 #pragma unroll
     for (int u = 0; u < NV; ++u)
-      if (tid + 256 * u < V) {
+      if (tid + NT * u < V) {
         const float e = expf(xr[u] - mx);
         se += e;
         if (!logsm) xr[u] = e;  // Softmax scores need only exp(x - max)
       }
   } else {
-    for (int c = tid; c < V; c += 256) se += expf(x[c] - mx);
+    for (int c = tid; c < V; c += NT) se += expf(x[c] - mx);
   }
-  se = block_sum(se, sh);
+  se = blk_sum<W>(se, sh);
   const float lse = logf(se), add = prev ? prev[r] : 0.f;
   float tv[KM];
   int ti[KM];
@@ -984,11 +1009,11 @@ __global__ void __launch_bounds__(256) beam_row_topk_kernel(const float* __restr
   if constexpr (NV > 0) {
 #pragma unroll
     for (int u = 0; u < NV; ++u) {
-      const int c = tid + 256 * u;
+      const int c = tid + NT * u;
       if (c < V) topk_insert<KM>(tv, ti, (logsm ? (xr[u] - mx) - lse : xr[u] / se) + add, j * V + c);
     }
   } else {
-    for (int c = tid; c < V; c += 256)
+    for (int c = tid; c < V; c += NT)
       topk_insert<KM>(tv, ti, (logsm ? (x[c] - mx) - lse : expf(x[c] - mx) / se) + add, j * V + c);
   }
   // the row's k best: k rounds of a wave argmax over the lanes' list heads (the winner pops its
@@ -1006,7 +1031,7 @@ __global__ void __launch_bounds__(256) beam_row_topk_kernel(const float* __restr
   }
   __syncthreads();
   if (wave == 0) {
-    const bool on = lane < 4 * k;
+    const bool on = lane < W * k;
     float v = on ? wv[lane / k][lane % k] : -INFINITY;
     int c = on ? wi[lane / k][lane % k] : 0x7fffffff;
     for (int sel = 0; sel < k; ++sel) {
@@ -1055,7 +1080,13 @@ __global__ void __launch_bounds__(64) beam_merge_kernel(const float* __restrict_
 template <int KM>
 static void beam_row_topk(const float* logits, const float* prev, int rows, int B, int V, int k, int logsm,
                           float* cand_v, int32_t* cand_i, hipStream_t s) {
-  if (V <= 256 * 40) beam_row_topk_kernel<KM, 40><<<rows, 256, 0, s>>>(logits, prev, B, V, k, logsm, cand_v, cand_i);
+  static const int nt = [] {  // threads per row (experiment knob CAPGEN_TOPK_THREADS: 256 or 512)
+    const char* e = std::getenv("CAPGEN_TOPK_THREADS");
+    return e ? std::atoi(e) : 256;
+  }();
+  if (nt == 512 && V <= 512 * 20 && KM * 8 <= 64)
+    beam_row_topk_kernel<KM, 20, 512><<<rows, 512, 0, s>>>(logits, prev, B, V, k, logsm, cand_v, cand_i);
+  else if (V <= 256 * 40) beam_row_topk_kernel<KM, 40><<<rows, 256, 0, s>>>(logits, prev, B, V, k, logsm, cand_v, cand_i);
   else beam_row_topk_kernel<KM, 0><<<rows, 256, 0, s>>>(logits, prev, B, V, k, logsm, cand_v, cand_i);
 }
 
