@@ -374,14 +374,14 @@ __device__ __forceinline__ void bf16x8_to_f(const uint4& u, float (&f)[8]) {
   }
 }
 template <int NIT>
-__global__ void __launch_bounds__(256) attn_decode_bf16_kernel(AttnGeom g, int G, bf16* __restrict__ o,
+__global__ void __launch_bounds__(512) attn_decode_bf16_kernel(AttnGeom g, int G, bf16* __restrict__ o,
                                                                float* __restrict__ probs) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, jr = lane >> 3, c = lane & 7;
   const bool group = G > 1;
   int b0, h, bk, qfirst, qstep;
-  if (group) {  // workgroup = (image, head); queries qi*nimg + image, qi = wv, wv + 4, ...
+  if (group) {  // workgroup = (image, head); queries qi*nimg + image, qi = wv, wv + waves, ...
     const int i = blockIdx.x / g.H;
-    h = blockIdx.x % g.H, bk = i, b0 = i, qfirst = wv, qstep = 4;
+    h = blockIdx.x % g.H, bk = i, b0 = i, qfirst = wv, qstep = blockDim.x >> 6;
   } else {
     const int w = blockIdx.x * 4 + wv;
     if (w >= g.B * g.H) return;  // no workgroup barrier in this kernel
@@ -479,9 +479,16 @@ static void launch_decode(const AttnGeom& g, T* o, float* probs, hipStream_t s) 
     if (((g.q_bs | g.k_bs | g.v_bs | g.k_ld | g.v_ld | g.o_bs) % 8) == 0) {
       const int blocks = grouped ? g.kv_bmod * g.H : (g.B * g.H + 3) / 4;
       const int Gk = grouped ? G : 1;
-      if (g.Lk <= 24) attn_decode_bf16_kernel<3><<<blocks, 256, 0, s>>>(g, Gk, o, probs);
-      else if (g.Lk <= 40) attn_decode_bf16_kernel<5><<<blocks, 256, 0, s>>>(g, Gk, o, probs);
-      else attn_decode_bf16_kernel<8><<<blocks, 256, 0, s>>>(g, Gk, o, probs);
+      // grouped: 4 waves share the image's queries (CAPGEN_DECODE_GROUP_WAVES = 1..8; one wave per
+      // beam row, 5 waves at beam 5, measured 25.1 vs 18.8 us)
+      static const int gw_env = [] {
+        const char* e = std::getenv("CAPGEN_DECODE_GROUP_WAVES");
+        return e ? std::max(1, std::min(8, std::atoi(e))) : 4;
+      }();
+      const int nt = grouped ? 64 * gw_env : 256;
+      if (g.Lk <= 24) attn_decode_bf16_kernel<3><<<blocks, nt, 0, s>>>(g, Gk, o, probs);
+      else if (g.Lk <= 40) attn_decode_bf16_kernel<5><<<blocks, nt, 0, s>>>(g, Gk, o, probs);
+      else attn_decode_bf16_kernel<8><<<blocks, nt, 0, s>>>(g, Gk, o, probs);
       CAPGEN_HIP(hipGetLastError());
       return;
     }
