@@ -66,3 +66,27 @@ def test_native_rewards_equal_python_restatement():
             nat = RewardScorer(idx, cider_reward_weight=1.0, bleu_reward_weight=1.0)
             assert nat.native and not py.native
             np.testing.assert_allclose(nat.scores(target, sample), py.scores(target, sample), rtol=1e-9, atol=1e-12)
+
+
+def test_native_rewards_packed_and_general_keys_agree():
+    """The native scorer packs n-grams into 64-bit keys when every token id (the "." id
+    included) is below 65534 and falls back to general keys otherwise; both give the same
+    rewards: the same token streams scored with ids shifted above 65534 (general path) and
+    as is (packed path), with the "." sentinel (no "." word) and with a real "." id."""
+    from capgen.scst import native_rewards
+    rng = np.random.default_rng(11)
+    B, L = 32, 12
+    target = rng.integers(3, 40, size=(B, L))
+    sample = rng.integers(0, 40, size=(B, L))
+    for b in range(B):
+        e = rng.integers(1, L + 1)
+        if e < L:
+            target[b, e] = 2
+            target[b, e + 1:] = 0
+    shift = 70000  # ids >= 3 moved above the 16-bit slot range; <NULL>/<START>/<END> keep theirs
+    t2 = np.where(target >= 3, target + shift, target)
+    s2 = np.where(sample >= 3, sample + shift, sample)
+    for dot in (-1, 5):
+        a = native_rewards(target, sample, 1, 2, 0, dot, 1.0, 1.0)
+        b = native_rewards(t2, s2, 1, 2, 0, dot + shift if dot >= 0 else -1, 1.0, 1.0)
+        np.testing.assert_allclose(a, b, rtol=1e-12, atol=1e-14)
