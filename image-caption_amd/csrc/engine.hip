@@ -1222,8 +1222,15 @@ struct capgen_engine {
     const int He = L.He, Hd = L.Hd, dke = d / He, dkd = dd / Hd;
     const bool on = fwd_drop;
     const float p = cfg.dropout, pa = cfg.attention_dropout;
-    // accumulated-gradient region (embedding table) and the striped LN/bias partials start at 0
-    CAPGEN_HIP(hipMemsetAsync(grads + L.n_dense, 0, (L.enc_lng - L.n_dense) * sizeof(float), s));
+    // the striped LN/bias partials start at 0 (the critical stream's first LayerNorm backward adds
+    // into them); the accumulated word-embedding gradient (20 MB at C2) is zeroed on es2 after the
+    // fork below -- its only writer is the embedding scatter on es2 (CAPGEN_EMB_MEMSET_SIDE=0: on s)
+    static const bool emb_side = [] {
+      const char* e = std::getenv("CAPGEN_EMB_MEMSET_SIDE");
+      return !(e && e[0] == '0');
+    }();
+    const bool emb_zero_side = emb_side && es2 != s && !L.has_img && !L.has_mf;
+    if (!emb_zero_side) CAPGEN_HIP(hipMemsetAsync(grads + L.n_dense, 0, (L.enc_lng - L.n_dense) * sizeof(float), s));
     CAPGEN_HIP(hipMemsetAsync(gstripe, 0, (size_t)NSTRIPE * n_small * sizeof(float), s));
     if (bstep) {
       adam_prepare(step, cfg.lr, cfg.beta1, cfg.beta2, adam_scal, s);
@@ -1262,6 +1269,7 @@ struct capgen_engine {
 
     // classifier: dlogits are unscaled (softmax - onehot); grad_scale folds 1/count (+focal)
     fork(s);
+    if (emb_zero_side) CAPGEN_HIP(hipMemsetAsync(grads + L.n_dense, 0, (L.enc_lng - L.n_dense) * sizeof(float), es2));
     column_sum(a.dlogits, Md, L.V, L.V, 1.f, a.grad_scale, GS(L.bc), act, es2, NSTRIPE, n_small);
     dw_side(a.dlogits, L.V, dec_out(), dd, L.Wc, dd, Md, L.V, dd, a.grad_scale, s);
     linear_dx(a.dlogits, L.V, L.Wc, dd, a.gOut, dd, Md, L.V, dd, 0, nullptr, a.grad_scale, s);
