@@ -190,6 +190,11 @@ struct capgen_engine {
   // [NSTRIPE][total - enc_lng]; folded into the gradient arena by stripe_reduce
   static constexpr int NSTRIPE = 16;
   float* gstripe = nullptr;
+  bool stripes_dirty = true;  // gstripe may hold partials (the next backward zeroes it first)
+  bool stripe_clear = [] {    // the folds zero the partials they read (CAPGEN_STRIPE_CLEAR=0: memset per step)
+    const char* e = std::getenv("CAPGEN_STRIPE_CLEAR");
+    return !(e && e[0] == '0');
+  }();
   int64_t n_small = 0;
   bool training = true;
   bool fwd_drop = true;  // dropout state of the last forward (backward must match)
@@ -1231,7 +1236,11 @@ struct capgen_engine {
     }();
     const bool emb_zero_side = emb_side && es2 != s && !L.has_img && !L.has_mf;
     if (!emb_zero_side) CAPGEN_HIP(hipMemsetAsync(grads + L.n_dense, 0, (L.enc_lng - L.n_dense) * sizeof(float), s));
-    CAPGEN_HIP(hipMemsetAsync(gstripe, 0, (size_t)NSTRIPE * n_small * sizeof(float), s));
+    // the striped partials are cleared by the previous backward's folds (stripe_reduce(clear)); a
+    // backward that did not reach both folds (diagnostic stops, errors) leaves them marked dirty
+    if (stripes_dirty || !stripe_clear) CAPGEN_HIP(hipMemsetAsync(gstripe, 0, (size_t)NSTRIPE * n_small * sizeof(float), s));
+    stripes_dirty = true;
+    int folds = 0;
     if (bstep) {
       adam_prepare(step, cfg.lr, cfg.beta1, cfg.beta2, adam_scal, s);
       zbuckets.clear();
@@ -1347,7 +1356,8 @@ struct capgen_engine {
       dw_launch(&wel, 1, es2);
       embedding_scatter_add(a.gE, a.ids, Md, L.dwe, cfg.pad_idx, G(L.emb), act, es2);
       // every decoder-side gradient is final here (in es2 order, after the fork above)
-      stripe_reduce(GS(L.dec_lng), NSTRIPE, n_small, L.total - L.dec_lng, G(L.dec_lng), 0, es2);
+      stripe_reduce(GS(L.dec_lng), NSTRIPE, n_small, L.total - L.dec_lng, G(L.dec_lng), 0, es2, stripe_clear);
+      ++folds;
     }
     // the encoder chain must not overwrite gO (read by the decoder-embedding branch on es2):
     // it runs on the other residual buffer and on tmp (free during backward)
@@ -1395,7 +1405,8 @@ struct capgen_engine {
     if (!bstep) join(s);  // queued bias column sums (es2) precede the fold below
     if (bstep) dep(s, ec, ev_b1);
     if (bstep && L.has_img) dep(es2, ec, ev_b2);
-    stripe_reduce(GS(L.enc_lng), NSTRIPE, n_small, L.dec_lng - L.enc_lng, G(L.enc_lng), 0, tail);
+    stripe_reduce(GS(L.enc_lng), NSTRIPE, n_small, L.dec_lng - L.enc_lng, G(L.enc_lng), 0, tail, stripe_clear);
+    if (++folds == 2) stripes_dirty = false;
     if (bstep) {
       bucket_update(0, L.enc[0].Wqkv, tail_grid);                   // feature/position embedding
       bucket_update(L.enc_lng, L.dec_lng - L.enc_lng, tail_grid);   // encoder LN / biases

@@ -70,9 +70,10 @@ void embedding_scatter_add(const void* dE, const int32_t* ids, int M, int d, int
 // db[n] += alpha (* *alpha_ptr) * sum_m X[m][n]
 void column_sum(const void* X, int M, int N, int64_t ldx, float alpha, const float* alpha_ptr, float* db,
                 DType t, hipStream_t s, int stripes = 1, int64_t stripe_stride = 0);
-// dst[i] (+)= sum_s S[s * stride + i], i < n  (folds striped partial sums)
-void stripe_reduce(const float* S, int stripes, int64_t stride, int64_t n, float* dst, int accumulate,
-                   hipStream_t s);
+// dst[i] (+)= sum_s S[s * stride + i], i < n  (folds striped partial sums); clear: the partials
+// are zeroed as they are read (the next backward then needs no memset of them)
+void stripe_reduce(float* S, int stripes, int64_t stride, int64_t n, float* dst, int accumulate,
+                   hipStream_t s, int clear = 0);
 // per-row cross entropy: loss_row[m] = lse - logit[tgt], dlogits = softmax - onehot (unscaled, 0 for pad)
 void cross_entropy_rows(const float* logits, const int32_t* tgt, int M, int V, int pad, float* loss_row,
                         void* dlogits, DType t, hipStream_t s);

@@ -484,19 +484,21 @@ void column_sum(const void* X, int M, int N, int64_t ldx, float alpha, const flo
   CAPGEN_HIP(hipGetLastError());
 }
 
-__global__ void stripe_reduce_kernel(const float* __restrict__ S, int stripes, int64_t stride, int64_t n,
-                                     float* __restrict__ dst, int accumulate) {
+__global__ void stripe_reduce_kernel(float* __restrict__ S, int stripes, int64_t stride, int64_t n,
+                                     float* __restrict__ dst, int accumulate, int clear) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     float acc = accumulate ? dst[i] : 0.f;
     for (int k = 0; k < stripes; ++k) acc += S[k * stride + i];
     dst[i] = acc;
+    if (clear)
+      for (int k = 0; k < stripes; ++k) S[k * stride + i] = 0.f;
   }
 }
-void stripe_reduce(const float* S, int stripes, int64_t stride, int64_t n, float* dst, int accumulate,
-                   hipStream_t s) {
+void stripe_reduce(float* S, int stripes, int64_t stride, int64_t n, float* dst, int accumulate, hipStream_t s,
+                   int clear) {
   if (n <= 0) return;
   int grid = (int)std::min<int64_t>((n + 255) / 256, 1024);
-  stripe_reduce_kernel<<<grid, 256, 0, s>>>(S, stripes, stride, n, dst, accumulate);
+  stripe_reduce_kernel<<<grid, 256, 0, s>>>(S, stripes, stride, n, dst, accumulate, clear);
   CAPGEN_HIP(hipGetLastError());
 }
 
