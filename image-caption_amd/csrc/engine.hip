@@ -772,10 +772,11 @@ struct capgen_engine {
     const int He = L.He, Hd = L.Hd, dke = d / He, dkd = dd / Hd;
     fB = B, fN = N, fT = T, fwd_drop = drop_on;
     const float p = cfg.dropout, pa = cfg.attention_dropout;
-    if (drop_on) bump_seed(seed, s);
 
     pack_encoder_input(feats, ft, pos, Me, L.F, L.P, L.Kp, a.Aenc, act, a.valid, s, in_idx, N, in_n_img);
-    prepare_captions(caps, B, T, cfg.pad_idx, a.ids, a.tgt, a.count, s);
+    // (+ the dropout seed advance when dropout is on: the pack kernel does not read the seed, every
+    // dropout site of this forward runs after this launch)
+    prepare_captions(caps, B, T, cfg.pad_idx, a.ids, a.tgt, a.count, s, drop_on ? seed : nullptr);
     if (comm) {
       if (count_override) {
         CAPGEN_HIP(hipMemcpyAsync(a.count, count_host, sizeof(float), hipMemcpyHostToDevice, s));
@@ -1242,7 +1243,12 @@ struct capgen_engine {
     stripes_dirty = true;
     int folds = 0;
     if (bstep) {
-      adam_prepare(step, cfg.lr, cfg.beta1, cfg.beta2, adam_scal, s);
+      // the step counter / bias corrections only feed the bucket stream's Adam: issue them there
+      // (off the critical stream) unless the step is being captured (ec joins a capture only
+      // through the buckets' events)
+      hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+      CAPGEN_HIP(hipStreamIsCapturing(s, &cst));
+      adam_prepare(step, cfg.lr, cfg.beta1, cfg.beta2, adam_scal, cst == hipStreamCaptureStatusNone ? ec : s);
       zbuckets.clear();
     }
     lns_next = 0;

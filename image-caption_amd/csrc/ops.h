@@ -60,7 +60,7 @@ void pack_encoder_input(const void* feats, DType feats_t, const float* pos, int 
                         int N = 0, int n_img = 0);
 // caps [B][T] -> ids_in [B][T-1], tgt [B][T-1]; count = #(tgt != pad) as f32   (model.py:88-89)
 void prepare_captions(const int32_t* caps, int B, int T, int pad, int32_t* ids_in, int32_t* tgt,
-                      float* count, hipStream_t s);
+                      float* count, hipStream_t s, uint64_t* seed_bump = nullptr);
 // out[m] = table[ids[m]] (f32 table -> T)                                      (model.py:432)
 void embedding_gather(const float* table, const int32_t* ids, int64_t ids_ld, int M, int d, void* out, DType t,
                       hipStream_t s);

@@ -366,9 +366,11 @@ void pack_encoder_input(const void* feats, DType ft, const float* pos, int M, in
 }
 
 __global__ void prep_caps_kernel(const int32_t* __restrict__ caps, int B, int T, int pad, int32_t* ids_in,
-                                 int32_t* tgt, float* count) {
+                                 int32_t* tgt, float* count, uint64_t* seed_bump) {
   __shared__ int cnt;
   if (threadIdx.x == 0) cnt = 0;
+  // the step's dropout seed advance (bump_seed) rides along: no kernel in this launch reads it
+  if (seed_bump && threadIdx.x == 0) *seed_bump += 0x9E3779B97F4A7C15ull;
   __syncthreads();
   const int L = T - 1;
   int local = 0;
@@ -385,8 +387,8 @@ __global__ void prep_caps_kernel(const int32_t* __restrict__ caps, int B, int T,
 }
 
 void prepare_captions(const int32_t* caps, int B, int T, int pad, int32_t* ids_in, int32_t* tgt, float* count,
-                      hipStream_t s) {
-  prep_caps_kernel<<<1, 1024, 0, s>>>(caps, B, T, pad, ids_in, tgt, count);
+                      hipStream_t s, uint64_t* seed_bump) {
+  prep_caps_kernel<<<1, 1024, 0, s>>>(caps, B, T, pad, ids_in, tgt, count, seed_bump);
   CAPGEN_HIP(hipGetLastError());
 }
 
