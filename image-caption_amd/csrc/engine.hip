@@ -773,10 +773,14 @@ struct capgen_engine {
     fB = B, fN = N, fT = T, fwd_drop = drop_on;
     const float p = cfg.dropout, pa = cfg.attention_dropout;
 
-    pack_encoder_input(feats, ft, pos, Me, L.F, L.P, L.Kp, a.Aenc, act, a.valid, s, in_idx, N, in_n_img);
     // (+ the dropout seed advance when dropout is on: the pack kernel does not read the seed, every
     // dropout site of this forward runs after this launch)
-    prepare_captions(caps, B, T, cfg.pad_idx, a.ids, a.tgt, a.count, s, drop_on ? seed : nullptr);
+    pack_encoder_input(feats, ft, pos, Me, L.F, L.P, L.Kp, a.Aenc, act, a.valid, s, in_idx, N, in_n_img,
+                       drop_on ? seed : nullptr);
+    // caption ids / targets / count: with the decoder front on es2 (and no count all-reduce, which
+    // stays on the critical stream) the prep runs there too, first thing of the front
+    const bool caps_front = overlap_front && es2 != s && !comm;
+    if (!caps_front) prepare_captions(caps, B, T, cfg.pad_idx, a.ids, a.tgt, a.count, s);
     if (comm) {
       if (count_override) {
         CAPGEN_HIP(hipMemcpyAsync(a.count, count_host, sizeof(float), hipMemcpyHostToDevice, s));
@@ -823,6 +827,7 @@ struct capgen_engine {
     if (front) {
       if (cap_split) cap_cut(s, 0, es2);
       else dep(s, es2, ev_ff);
+      if (caps_front) prepare_captions(caps, B, T, cfg.pad_idx, a.ids, a.tgt, a.count, es2);
       dec_embed(a.tmpf, es2);
       dec_self_half(0, a.tmpf, es2);
       if (cap_split) cap_cut(es2, 1, s);

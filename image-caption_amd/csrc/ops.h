@@ -57,7 +57,7 @@ void layernorm_param_sums(const LnBwd& a, DType t, hipStream_t s);
 // (indices outside [0, n_img) give all-padding rows)
 void pack_encoder_input(const void* feats, DType feats_t, const float* pos, int M, int F, int P, int Kp,
                         void* out, DType out_t, uint8_t* valid, hipStream_t s, const int32_t* img_idx = nullptr,
-                        int N = 0, int n_img = 0);
+                        int N = 0, int n_img = 0, uint64_t* seed_bump = nullptr);
 // caps [B][T] -> ids_in [B][T-1], tgt [B][T-1]; count = #(tgt != pad) as f32   (model.py:88-89)
 void prepare_captions(const int32_t* caps, int B, int T, int pad, int32_t* ids_in, int32_t* tgt,
                       float* count, hipStream_t s, uint64_t* seed_bump = nullptr);

@@ -306,10 +306,13 @@ void layernorm_bwd(const LnBwd& a_in, DType t, hipStream_t s) {
 template <typename TI, typename TO>
 __global__ void __launch_bounds__(256) pack_kernel(const TI* __restrict__ feats, const float* __restrict__ pos,
                                                    const int32_t* __restrict__ img_idx, int n_img, int N, int F, int P,
-                                                   int Kp, TO* __restrict__ out, uint8_t* __restrict__ valid) {
+                                                   int Kp, TO* __restrict__ out, uint8_t* __restrict__ valid,
+                                                   uint64_t* seed_bump) {
   constexpr int V = 16 / sizeof(TI);  // one 16-B load of features per step
   __shared__ int nz;
   const int m = blockIdx.x;
+  // the step's dropout seed advance rides along: nothing in this launch reads the seed
+  if (seed_bump && m == 0 && threadIdx.x == 0) *seed_bump += 0x9E3779B97F4A7C15ull;
   // row m = (b, n) of the batch; with img_idx the features / positions of image img_idx[b] are
   // read straight from an HBM-resident store (dataset.py:12-18 + DataLoader collate, fused)
   int64_t src = m;
@@ -349,19 +352,20 @@ __global__ void __launch_bounds__(256) pack_kernel(const TI* __restrict__ feats,
 }
 
 void pack_encoder_input(const void* feats, DType ft, const float* pos, int M, int F, int P, int Kp, void* out,
-                        DType ot, uint8_t* valid, hipStream_t s, const int32_t* img_idx, int N, int n_img) {
+                        DType ot, uint8_t* valid, hipStream_t s, const int32_t* img_idx, int N, int n_img,
+                        uint64_t* seed_bump) {
   if (M <= 0) return;
   require(F % 8 == 0 && ((uintptr_t)feats & 15) == 0, "pack: feature width must be a multiple of 8, 16-B aligned");
   require(img_idx == nullptr || N > 0, "pack: indexed gather needs N");
   dim3 grid(M);
   if (ft == DType::F32 && ot == DType::F32)
-    pack_kernel<float, float><<<grid, 256, 0, s>>>((const float*)feats, pos, img_idx, n_img, N, F, P, Kp, (float*)out, valid);
+    pack_kernel<float, float><<<grid, 256, 0, s>>>((const float*)feats, pos, img_idx, n_img, N, F, P, Kp, (float*)out, valid, seed_bump);
   else if (ft == DType::F32 && ot == DType::BF16)
-    pack_kernel<float, bf16><<<grid, 256, 0, s>>>((const float*)feats, pos, img_idx, n_img, N, F, P, Kp, (bf16*)out, valid);
+    pack_kernel<float, bf16><<<grid, 256, 0, s>>>((const float*)feats, pos, img_idx, n_img, N, F, P, Kp, (bf16*)out, valid, seed_bump);
   else if (ft == DType::BF16 && ot == DType::BF16)
-    pack_kernel<bf16, bf16><<<grid, 256, 0, s>>>((const bf16*)feats, pos, img_idx, n_img, N, F, P, Kp, (bf16*)out, valid);
+    pack_kernel<bf16, bf16><<<grid, 256, 0, s>>>((const bf16*)feats, pos, img_idx, n_img, N, F, P, Kp, (bf16*)out, valid, seed_bump);
   else
-    pack_kernel<bf16, float><<<grid, 256, 0, s>>>((const bf16*)feats, pos, img_idx, n_img, N, F, P, Kp, (float*)out, valid);
+    pack_kernel<bf16, float><<<grid, 256, 0, s>>>((const bf16*)feats, pos, img_idx, n_img, N, F, P, Kp, (float*)out, valid, seed_bump);
   CAPGEN_HIP(hipGetLastError());
 }
 
