@@ -485,7 +485,19 @@ def test_grouped_weight_gradients_match_single_launches_bf16(monkeypatch):
     ga, gb = a.grads_state_dict(), b.grads_state_dict()
     rel = {n: ((ga[n].double() - gb[n].double()).norm() / (ga[n].double().norm() + 1e-12)).item() for n in ga}
     bad = {n: r for n, r in rel.items() if r >= 1e-4}
-    assert not bad, (len(bad), len(rel), sorted(bad.items(), key=lambda kv: -kv[1])[:8])
+    if bad:  # diagnostics for the rare mismatch: which engine is the odd one out?
+        d = _engine(cfg, seed, dtype="bf16", dropout=0.3)  # a second grouped engine, run alone
+        d.set_training(True)
+        d.set_rng_seed(5)
+        torch.cuda.synchronize()
+        d.forward(f, p, c)
+        d.backward()
+        gd = d.grads_state_dict()
+        worst = max(bad, key=bad.get)
+        far = lambda g: ((g[worst].double() - gd[worst].double()).norm() / (gd[worst].double().norm() + 1e-12)).item()
+        bad = (bad, f"{worst}: single-launch engine vs a fresh grouped one {far(ga):.2e}, "
+                    f"grouped vs the fresh grouped one {far(gb):.2e}")
+    assert not bad, (len(rel), bad if isinstance(bad, tuple) else sorted(bad.items(), key=lambda kv: -kv[1])[:8])
 
 
 @pytest.mark.parametrize("graph", [False, True])
