@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcapgen.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 F32, BF16 = 0, 1
 
@@ -86,6 +86,12 @@ _SIGS = {
     "capgen_dp_sync_adam_state": (C.c_int, [_P]),
     "capgen_dp_buckets": (C.c_int, [_P, _P, _P, C.c_int, _P]),
     "capgen_dp_debug_shard": (C.c_int, [_P, C.c_int, C.c_int]),
+    "capgen_tune_load": (C.c_int, [C.c_char_p]),
+    "capgen_tune_save": (C.c_int, [C.c_char_p]),
+    "capgen_tune_live_count": (C.c_int, []),
+    "capgen_debug_hazard": (C.c_int, [C.c_int, C.c_char_p, C.c_int, C.POINTER(C.c_int)]),
+    "capgen_debug_side_delay": (C.c_int, [C.c_double]),
+    "capgen_debug_collectives": (C.c_int, [_P, C.c_int, C.c_char_p, C.c_int]),
     "capgen_scst_rewards": (C.c_int, [_P, C.c_int64, _P, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                       C.c_int64, C.c_double, C.c_double, _P]),
 }
@@ -151,3 +157,46 @@ def param_table(cfg):
     check(lib.capgen_param_table(C.byref(c), arr, n.value, C.byref(n), C.byref(total)))
     out = [(p.name.decode(), p.ndim, p.rows, p.cols, p.offset, p.row_stride) for p in arr]
     return out, total.value
+
+
+TUNE_TABLE = os.path.join(_HERE, "tune_gfx950.txt")
+
+
+def tune_save(path: str = TUNE_TABLE) -> int:
+    """Write every GEMM autotune choice this process knows (tuned or loaded) to `path`."""
+    n = load().capgen_tune_save(path.encode())
+    if n < 0:
+        check(1)
+    return n
+
+
+def tune_load(path: str) -> int:
+    """Merge a persisted autotune table (-1: no such file)."""
+    return load().capgen_tune_load(path.encode())
+
+
+def tune_live_count() -> int:
+    """GEMM shapes this process tuned live (0 when the persisted table covered every shape)."""
+    return load().capgen_tune_live_count()
+
+
+def hazard_start() -> None:
+    """Start logging every launch / event / host sync of the engines (clears the log)."""
+    check(load().capgen_debug_hazard(1, None, 0, None))
+
+
+def hazard_stop() -> None:
+    check(load().capgen_debug_hazard(0, None, 0, None))
+
+
+def hazard_check(cap: int = 8192):
+    """(number of unordered conflicting launch pairs since hazard_start, report text)."""
+    buf = C.create_string_buffer(cap)
+    n = C.c_int(0)
+    check(load().capgen_debug_hazard(2, buf, cap, C.byref(n)))
+    return n.value, buf.value.decode(errors="replace")
+
+
+def side_delay(us: float) -> None:
+    """Spin `us` microseconds in front of every launch off the critical stream (0 = off)."""
+    check(load().capgen_debug_side_delay(float(us)))

@@ -293,6 +293,12 @@ class Engine:
                                               cnts.ctypes.data_as(C.c_void_p), cap, C.byref(n)))
         return [(int(offs[i]), int(cnts[i])) for i in range(n.value)]
 
+    def collectives_log(self, op: int, cap: int = 1 << 16) -> str:
+        """Test hook: 1 = start recording the engine's RCCL calls, 0 = stop, 2 = the recorded calls."""
+        buf = C.create_string_buffer(cap)
+        _lib.check(self.lib.capgen_debug_collectives(self.h, int(op), buf, cap))
+        return buf.value.decode()
+
     def dp_debug_shard(self, rank: int, world: int):
         """Test hook: update as rank `rank` of `world` would under the sharded update, no collectives."""
         _lib.check(self.lib.capgen_dp_debug_shard(self.h, int(rank), int(world)))

@@ -38,6 +38,11 @@ class HostBatchStager:
         self.caps = torch.empty((B, T), dtype=torch.int32, device=dev)  # fixed pointers for the graph
         self.idx = torch.empty((B,), dtype=torch.int32, device=dev)
         self.copy_stream = torch.cuda.Stream(dev)
+        # A stager replaces another when the batch shape changes (main.py's last, smaller batch of an
+        # epoch): the buffers above may reuse memory the caching allocator got back from the old
+        # stager while a step issued on the current stream may still read it.  Every H2D of this
+        # stager runs on copy_stream, so make it wait for everything issued so far on that stream.
+        self.copy_stream.wait_stream(torch.cuda.current_stream(dev))
         self.h2d_done = [torch.cuda.Event() for _ in range(S)]
         self.consumed = [torch.cuda.Event() for _ in range(S)]
         self.i = 0

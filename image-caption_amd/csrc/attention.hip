@@ -13,10 +13,12 @@
 // Semantics (modules.py:16-27, 67-92): s = (q / temperature) . k^T; masked_fill(-inf);
 // softmax; dropout; o = p . v.  Backward recomputes the dropout mask from the counter RNG.
 #include <cstdlib>
+#include <algorithm>
 
 #include <type_traits>
 
 #include "attention.h"
+#include "hazard.h"
 
 namespace capgen {
 
@@ -553,9 +555,28 @@ static void allow_big_lds(K kernel) {
   }
 }
 
+// the device bytes one attention launch touches (hazard checker, hazard.h)
+static void hz_attention(const AttnGeom& g, DType t, hipStream_t s, const char* name, const void* o, const float* probs,
+                         const void* dout, const void* dq, const void* dk, const void* dv) {
+  using namespace hz;
+  const int64_t e = dsize(t), w = (int64_t)g.H * g.dk;
+  const int Bk = g.kv_bmod > 0 ? std::min(g.B, g.kv_bmod) : g.B;
+  const Rgn r[] = {
+      rows_blk(g.q, g.B, g.Lq, g.q_bs, g.q_ld, w, e, RD), rows_blk(g.k, Bk, g.Lk, g.k_bs, g.k_ld, w, e, RD),
+      rows_blk(g.v, Bk, g.Lk, g.v_bs, g.v_ld, w, e, RD), blk(g.key_valid, Bk, g.Lk, g.kv_bs, RD),
+      blk(g.key_ids, Bk, (int64_t)g.Lk * 4, g.kid_bs * 4, RD), rd(g.drop.seed_ptr, 8),
+      rows_blk(o, g.B, g.Lq, g.o_bs, g.o_ld, w, e, WR),
+      rd(probs, dout ? (int64_t)g.B * g.H * g.Lq * g.Lk * 4 : 0),  // backward reads the saved probabilities
+      wr(dout ? nullptr : probs, (int64_t)g.B * g.H * g.Lq * g.Lk * 4),
+      rows_blk(dout, g.B, g.Lq, g.o_bs, g.o_ld, w, e, RD), rows_blk(dq, g.B, g.Lq, g.q_bs, g.q_ld, w, e, WR),
+      rows_blk(dk, Bk, g.Lk, g.k_bs, g.k_ld, w, e, WR), rows_blk(dv, Bk, g.Lk, g.v_bs, g.v_ld, w, e, WR)};
+  op(s, name, r, sizeof r / sizeof r[0]);
+}
+
 void attention_fwd(const AttnGeom& g, void* o, float* probs, DType t, hipStream_t s) {
   if (skip_mask() & 2) return;
   check_geom(g);
+  if (hz::active() && !g.kv_row) hz_attention(g, t, s, "attention_fwd", o, probs, nullptr, nullptr, nullptr, nullptr);
   if (g.Lq == 1 && g.dk == 64 && g.drop.seed_ptr == nullptr && g.q_ld % 8 == 0 && g.k_ld % 8 == 0 &&
       ((g.q_bs | g.k_bs) % 8) == 0) {  // KV-cached decode step
     if (t == DType::F32) launch_decode<float>(g, (float*)o, probs, s);
@@ -580,6 +601,7 @@ void attention_bwd(const AttnGeom& g, const float* probs, const void* dout, void
                    hipStream_t s) {
   if (skip_mask() & 8) return;
   check_geom(g);
+  if (hz::active()) hz_attention(g, t, s, "attention_bwd", nullptr, probs, dout, dq, dk, dv);
   if (t == DType::BF16 && attention_mfma_ok(g))
     return attention_bwd_mfma(g, (const bf16*)dout, (bf16*)dq, (bf16*)dk, (bf16*)dv, s);
   const size_t smem = bwd_smem(g);

@@ -25,6 +25,7 @@
 #include "../../include/capgen.h"
 #include "attention.h"
 #include "gemm.h"
+#include "hazard.h"
 #include "layout.h"
 #include "ops.h"
 #include "variants.h"
@@ -221,13 +222,14 @@ struct capgen_engine {
   // overlapped, but without the profiler the single graph measured faster (4-round A/B: 3.032 vs
   // 3.048 ms/step; front off: 3.072).  The multi-branch graph costs the host more to launch
   // (enqueue per step 2.52 vs 2.27 ms; linear graphs ~0.1 us per node), which matters once the
-  // step also issues the per-bucket collectives: split by default under DP with world > 1 only
-  // (CAPGEN_FWD_SPLIT=0/1 forces either)
+  // step also issues the per-bucket collectives.  The single graph is the default at every world
+  // size (faster on the GPU; the count / partial-CE all-reduces capture into it as well);
+  // CAPGEN_FWD_SPLIT=1 selects the split graphs
   int fwd_split_env = [] {
     const char* e = std::getenv("CAPGEN_FWD_SPLIT");
     return e ? (e[0] == '1' ? 1 : 0) : -1;
   }();
-  bool fwd_split() const { return fwd_split_env == 1 || (fwd_split_env < 0 && comm && world > 1); }
+  bool fwd_split() const { return fwd_split_env == 1; }
   bool cap_split = false;  // forward() is being captured in split mode: it ends/begins captures
   hipGraph_t fg[4] = {};   // pre, front, encoder, decoder
   hipGraphExec_t fx[4] = {};
@@ -243,9 +245,9 @@ struct capgen_engine {
     CAPGEN_HIP(hipGraphLaunch(fx[0], cs));
     dep(cs, es2, ev_ff);
     CAPGEN_HIP(hipGraphLaunch(fx[1], es2));
-    CAPGEN_HIP(hipEventRecord(ev_fj, es2));
+    hz::record(ev_fj, es2);
     CAPGEN_HIP(hipGraphLaunch(fx[2], cs));
-    CAPGEN_HIP(hipStreamWaitEvent(cs, ev_fj, 0));
+    hz::wait(cs, ev_fj);
     CAPGEN_HIP(hipGraphLaunch(fx[3], cs));
   }
   bool have_fwd_graph() const { return fexec || fx[3]; }
@@ -284,6 +286,10 @@ struct capgen_engine {
     return e ? std::atoi(e) : 1;
   }();
   int zemu_rank = 0, zemu_world = 1;  // capgen_dp_debug_shard: shard as rank r of w, no collectives
+  // set by the sharded update: the Adam moments (resp. the gradient arena) are current in this rank's
+  // chunks only until capgen_dp_sync_adam_state (resp. the next backward) -- the whole-arena getters
+  // refuse them in between instead of returning stale data
+  bool moments_sharded = false, grads_sharded = false;
   std::vector<std::array<int64_t, 2>> zbuckets;  // this step's bucket ranges, in issue order
   bool zbuckets_checked = false;
   int zworld() const {
@@ -517,9 +523,9 @@ struct capgen_engine {
     p.take(a.rl_scal, 8);
     const int64_t dmax = std::max<int64_t>(std::max(d, dd), L_().dwe);
     T_(a.tmp, Mx * dmax);
-    a.lns.resize(kLnSideSlots);
+    a.lns.resize(ln_sums_side ? kLnSideSlots : 0);  // (~90 MB at C2: only for the CAPGEN_LN_SUMS_SIDE experiment)
     for (auto& x : a.lns) T_(x, Mx * dmax);
-    a.lns_cap = (int64_t)Mx * dmax;
+    a.lns_cap = ln_sums_side ? (int64_t)Mx * dmax : 0;
     T_(a.gOut, Mx * dmax);
     T_(a.gRes, Mx * dmax);
     T_(a.gKV, Me * L_().Ld * 2 * dd);
@@ -598,7 +604,7 @@ struct capgen_engine {
     if (ws && B <= a.B && N <= a.N && T <= a.T) return;
     int nB = std::max(B, a.B), nN = std::max(N, a.N), nT = std::max(T, a.T);
     if (ws) {
-      CAPGEN_HIP(hipStreamSynchronize(es));
+      hz::host_sync(es);
       CAPGEN_HIP(hipFree(ws));
       ws = nullptr;
       drop_graph();
@@ -783,11 +789,14 @@ struct capgen_engine {
     if (!caps_front) prepare_captions(caps, B, T, cfg.pad_idx, a.ids, a.tgt, a.count, s);
     if (comm) {
       if (count_override) {
+        if (hz::active()) hz::op(s, "count_copy", {hz::wr(a.count, 4)});
         CAPGEN_HIP(hipMemcpyAsync(a.count, count_host, sizeof(float), hipMemcpyHostToDevice, s));
-        CAPGEN_HIP(hipEventRecord(ev_count, s));  // capgen_dp_set_global_count waits for this copy
+        hz::record(ev_count, s);  // capgen_dp_set_global_count waits for this copy
       }
-      else
+      else {
+        nccl_op(s, "allreduce(count)", a.count, 4);
         NCCL_CHECK(ncclAllReduce(a.count, a.count, 1, ncclFloat, ncclSum, comm, s));
+      }
     }
 
     // ---- decoder front (model.py:432-436 and block 0's self-attention half + cross query,
@@ -797,7 +806,7 @@ struct capgen_engine {
     dmask.ids = a.ids, dmask.pad_idx = cfg.pad_idx;
     const bool front = overlap_front && es2 != s;
     auto dec_embed = [&](void* tmp, hipStream_t fs) {
-      embedding_gather(P(L.emb), a.ids, 1, Md, L.dwe, a.E, act, fs);
+      embedding_gather(P(L.emb), a.ids, 1, Md, L.dwe, a.E, act, fs, L.V);
       LnFwd ln;
       ln.M = Md, ln.d = dd, ln.a = tmp, ln.pe = pe, ln.pe_L = Lq, ln.gamma = P(L.dec_lng), ln.beta = P(L.dec_lnb);
       ln.y = a.D[0], ln.v_save = a.dv0, ln.mean = a.dm0, ln.rstd = a.dr0;
@@ -831,7 +840,7 @@ struct capgen_engine {
       dec_embed(a.tmpf, es2);
       dec_self_half(0, a.tmpf, es2);
       if (cap_split) cap_cut(es2, 1, s);
-      else CAPGEN_HIP(hipEventRecord(ev_fj, es2));
+      else hz::record(ev_fj, es2);
     }
 
     // ---- encoder (model.py:294-332) ----
@@ -854,19 +863,19 @@ struct capgen_engine {
       dep(s, es2, ev_ff);
       linear(a.X[L.Le], d, L.Wkv_all + (int64_t)nkv0 * d, d, at(a.KV, nkv0), (int64_t)L.Ld * 2 * dd, act, Me,
              (L.Ld - 1) * 2 * dd, d, nullptr, 0, es2);
-      CAPGEN_HIP(hipEventRecord(ev_kv, es2));
+      hz::record(ev_kv, es2);
     }
 
     // ---- decoder (model.py:419-459) ----
     if (front && cap_split) cap_cut(s, 2, s);
-    else if (front) CAPGEN_HIP(hipStreamWaitEvent(s, ev_fj, 0));
+    else if (front) hz::wait(s, ev_fj);
     else dec_embed(a.tmp, s);
     const int64_t kvld = (int64_t)L.Ld * 2 * dd;
     for (int l = 0; l < L.Ld; ++l) {
       const auto& w = L.dec[l];
       auto& A = a.dec[l];
       if (!(front && l == 0)) dec_self_half(l, a.tmp, s);
-      if (kvs && l == 1) CAPGEN_HIP(hipStreamWaitEvent(s, ev_kv, 0));
+      if (kvs && l == 1) hz::wait(s, ev_kv);
       // cross attention over the encoder output, context mask = region key-pad (model.py:82)
       AttnGeom c;
       c.B = B, c.H = Hd, c.Lq = Lq, c.Lk = N, c.dk = dkd;
@@ -913,6 +922,7 @@ struct capgen_engine {
       // partial sums / global count -- one 4-byte all-reduce, then the (Focal) loss and the
       // gradient scale from it on every rank (FocalLoss transforms the global mean, loss.py:20-28)
       loss_finalize(a.loss_row, Md, a.count, 0, a.loss_ce, nullptr, s, nullptr, /*partial=*/1);
+      nccl_op(s, "allreduce(ce)", a.loss_ce, 4);
       NCCL_CHECK(ncclAllReduce(a.loss_ce, a.loss_ce, 1, ncclFloat, ncclSum, comm, s));
       loss_finalize(nullptr, 0, a.count, cfg.focal_loss, lo, a.grad_scale, s, a.loss_ce);
     } else {
@@ -927,14 +937,35 @@ struct capgen_engine {
   // `to` waits for everything issued so far on `from` (no-op when they are one stream)
   static void dep(hipStream_t from, hipStream_t to, hipEvent_t e) {
     if (from == to) return;
-    CAPGEN_HIP(hipEventRecord(e, from));
-    CAPGEN_HIP(hipStreamWaitEvent(to, e, 0));
+    hz::record(e, from);
+    hz::wait(to, e);
+  }
+  static void memset_async(void* p, size_t bytes, hipStream_t s) {
+    if (hz::active()) hz::op(s, "memset", {hz::wr(p, (int64_t)bytes)});
+    CAPGEN_HIP(hipMemsetAsync(p, 0, bytes, s));
+  }
+  // an RCCL collective on s, in place over [p, p + bytes): hazard log + the collective log
+  // (capgen_debug_collectives: every rank must issue the same sequence, or the job hangs)
+  bool coll_log_on = false;
+  std::vector<std::string> coll_log;
+  void nccl_op(hipStream_t s, const char* name, const void* p, int64_t bytes) {
+    if (hz::g_log) hz::op(s, name, {hz::wr(p, bytes)});
+    if (coll_log_on) {
+      const char* role = s == ec ? "bucket" : s == es2 ? "side" : "critical";
+      coll_log.push_back(std::string(name) + " " + std::to_string(bytes) + " B on " + role);
+    }
   }
   void fork(hipStream_t s) { dep(s, es2, ev_fork); }
   void join(hipStream_t s) {
     flush(s);
-    dep(es2, s, ev_join);
+    if (!dbg_drop_join) dep(es2, s, ev_join);
   }
+  // hazard-checker self-test (CAPGEN_DEBUG_DROP_JOIN=1): the side stream is never joined back --
+  // a deliberately missing edge the checker must report (results are then racy: test use only)
+  bool dbg_drop_join = [] {
+    const char* e = std::getenv("CAPGEN_DEBUG_DROP_JOIN");
+    return e && e[0] == '1';
+  }();
   // Weight-gradient GEMMs are queued and issued on es2 in one batch per block (flush): an event
   // record/wait pair costs the recording stream ~7 us of bubble on ROCm 7 (tools/kprobe.hip:
   // 13 us per eager fork/join pair), so the critical stream records one event per block instead
@@ -1011,7 +1042,7 @@ struct capgen_engine {
     lns_pending.clear();
     for (const SideGemm& j : nn_pending) {
       gemm(j.ga, act, DType::F32, false, true, es2);
-      if (j.mark) CAPGEN_HIP(hipEventRecord(ev_part, es2));
+      if (j.mark) hz::record(ev_part, es2);
     }
     nn_pending.clear();
   }
@@ -1132,17 +1163,28 @@ struct capgen_engine {
     const int zw = zworld();
     if (zsharded() && n % (4 * zw) == 0) {  // sharded update (ZeRO-1); buckets are 64-element aligned
       const int64_t c = n / zw, o = off + (int64_t)zrank() * c;
+      if (zw > 1) moments_sharded = true;  // this rank's moments are current in its chunks only
+      if (comm && zw > 1) grads_sharded = true;  // the gradient arena holds reduce-scattered chunks
       // in place: rank r's chunk of the summed gradients lands at grads + o
-      if (comm) NCCL_CHECK(ncclReduceScatter(grads + off, grads + o, (size_t)c, ncclFloat, ncclSum, comm, ec));
+      if (comm) {
+        nccl_op(ec, "reduce_scatter", grads + off, n * 4);
+        NCCL_CHECK(ncclReduceScatter(grads + off, grads + o, (size_t)c, ncclFloat, ncclSum, comm, ec));
+      }
       const int64_t ns = shadow ? std::max<int64_t>(0, std::min(n, L.n_dense - off)) : 0;
       adam_update(params + o, grads + o, am + o, av + o, (size_t)c, cfg.beta1, cfg.beta2, cfg.eps, adam_scal, nullptr, 0,
                   ec, grid_cap);
       // in place: every rank's updated chunk -> params + off (sendbuff = recvbuff + rank * c)
-      if (comm) NCCL_CHECK(ncclAllGather(params + o, params + off, (size_t)c, ncclFloat, comm, ec));
+      if (comm) {
+        nccl_op(ec, "all_gather", params + off, n * 4);
+        NCCL_CHECK(ncclAllGather(params + o, params + off, (size_t)c, ncclFloat, comm, ec));
+      }
       if (ns > 0) to_bf16(params + off, shadow + off, (size_t)ns, ec);
       return;
     }
-    if (comm) NCCL_CHECK(ncclAllReduce(grads + off, grads + off, (size_t)n, ncclFloat, ncclSum, comm, ec));
+    if (comm) {
+        nccl_op(ec, "allreduce(bucket)", grads + off, n * 4);
+        NCCL_CHECK(ncclAllReduce(grads + off, grads + off, (size_t)n, ncclFloat, ncclSum, comm, ec));
+      }
     adam_range(off, n, ec, grid_cap);
   }
   // once: the step's buckets cover the arena exactly (each element updated by exactly one bucket)
@@ -1229,6 +1271,7 @@ struct capgen_engine {
   void backward(hipStream_t s, bool step_params = false) {
     bstep = step_params;
     require(fB > 0, "backward: call forward first");
+    grads_sharded = false;
     const int B = fB, N = fN, Lq = fT - 1, Me = B * N, Md = B * Lq, d = L.d, dd = L.dd;
     const int He = L.He, Hd = L.Hd, dke = d / He, dkd = dd / Hd;
     const bool on = fwd_drop;
@@ -1241,10 +1284,10 @@ struct capgen_engine {
       return !(e && e[0] == '0');
     }();
     const bool emb_zero_side = emb_side && es2 != s && !L.has_img && !L.has_mf;
-    if (!emb_zero_side) CAPGEN_HIP(hipMemsetAsync(grads + L.n_dense, 0, (L.enc_lng - L.n_dense) * sizeof(float), s));
+    if (!emb_zero_side) memset_async(grads + L.n_dense, (L.enc_lng - L.n_dense) * sizeof(float), s);
     // the striped partials are cleared by the previous backward's folds (stripe_reduce(clear)); a
     // backward that did not reach both folds (diagnostic stops, errors) leaves them marked dirty
-    if (stripes_dirty || !stripe_clear) CAPGEN_HIP(hipMemsetAsync(gstripe, 0, (size_t)NSTRIPE * n_small * sizeof(float), s));
+    if (stripes_dirty || !stripe_clear) memset_async(gstripe, (size_t)NSTRIPE * n_small * sizeof(float), s);
     stripes_dirty = true;
     int folds = 0;
     if (bstep) {
@@ -1289,7 +1332,7 @@ struct capgen_engine {
 
     // classifier: dlogits are unscaled (softmax - onehot); grad_scale folds 1/count (+focal)
     fork(s);
-    if (emb_zero_side) CAPGEN_HIP(hipMemsetAsync(grads + L.n_dense, 0, (L.enc_lng - L.n_dense) * sizeof(float), es2));
+    if (emb_zero_side) memset_async(grads + L.n_dense, (L.enc_lng - L.n_dense) * sizeof(float), es2);
     column_sum(a.dlogits, Md, L.V, L.V, 1.f, a.grad_scale, GS(L.bc), act, es2, NSTRIPE, n_small);
     dw_side(a.dlogits, L.V, dec_out(), dd, L.Wc, dd, Md, L.V, dd, a.grad_scale, s);
     linear_dx(a.dlogits, L.V, L.Wc, dd, a.gOut, dd, Md, L.V, dd, 0, nullptr, a.grad_scale, s);
@@ -1365,7 +1408,7 @@ struct capgen_engine {
       linear_dx(a.gAd, dd, L.Wel, L.dwe, a.gE, L.dwe, Md, dd, L.dwe, 0, nullptr, nullptr, es2);
       const DwJob wel{a.gAd, a.E, dd, L.dwe, L.Wel, L.dwe, Md, dd, L.dwe, nullptr};
       dw_launch(&wel, 1, es2);
-      embedding_scatter_add(a.gE, a.ids, Md, L.dwe, cfg.pad_idx, G(L.emb), act, es2);
+      embedding_scatter_add(a.gE, a.ids, Md, L.dwe, cfg.pad_idx, G(L.emb), act, es2, L.V);
       // every decoder-side gradient is final here (in es2 order, after the fork above)
       stripe_reduce(GS(L.dec_lng), NSTRIPE, n_small, L.total - L.dec_lng, G(L.dec_lng), 0, es2, stripe_clear);
       ++folds;
@@ -1375,7 +1418,7 @@ struct capgen_engine {
     gO = eO;
     gR = a.tmp;
     if (split_kv) {  // block 0's term + the f32 sum of blocks Ld-1 .. 1 (summed on es2)
-      CAPGEN_HIP(hipStreamWaitEvent(s, ev_part, 0));
+      hz::wait(s, ev_part);
       GemmArgs ga = dx_args(a.gKV, kvld, L.Wkv_all, d, gO, d, Me, 2 * dd, d, 0);
       ga.cin = a.gEnc32, ga.ldcin = d, ga.prio = prio(s);
       gemm(ga, act, act, false, true, s);
@@ -1432,6 +1475,7 @@ struct capgen_engine {
 
   void allreduce_grads(hipStream_t s) {
     if (!comm) return;
+    nccl_op(s, "allreduce(grads)", grads, L.total * 4);
     NCCL_CHECK(ncclAllReduce(grads, grads, (size_t)L.total, ncclFloat, ncclSum, comm, s));
   }
 
@@ -1448,26 +1492,30 @@ struct capgen_engine {
   // ------------------------------------------------------------------------------------
   // stream hand-off: caller stream -> engine stream -> caller stream
   void enter(hipStream_t cs) {
-    CAPGEN_HIP(hipEventRecord(ev_in, cs));
-    CAPGEN_HIP(hipStreamWaitEvent(es, ev_in, 0));
+    hz::record(ev_in, cs);
+    hz::wait(es, ev_in);
+    hz::set_critical(es);
   }
   void leave(hipStream_t cs) {
-    CAPGEN_HIP(hipEventRecord(ev_out, es));
-    CAPGEN_HIP(hipStreamWaitEvent(cs, ev_out, 0));
+    hz::record(ev_out, es);
+    hz::wait(cs, ev_out);
   }
 
   void train_step(const void* f, DType ft, const float* pos, const int32_t* caps, int B, int N, int T, float* loss,
                   hipStream_t cs) {
     ensure_acts(B, N, T);
     Key k{f, pos, caps, loss, (int)ft, B, N, T, training, in_idx, in_n_img};
-    if (direct_on && !graph_on && fwd_graph_on && !count_override && have_fwd_graph() && fkey == k && cs != es) {
+    // (the hazard checker's log runs the eager forward: the graph replays the same launches)
+    const bool fwd_graph = fwd_graph_on && !hz::g_log;
+    if (direct_on && !graph_on && fwd_graph && !count_override && have_fwd_graph() && fkey == k && cs != es) {
       crit = cs;
+      hz::set_critical(cs);
       launch_fwd(cs);
       fB = B, fN = N, fT = T, fwd_drop = training;  // host state forward() would have set
       backward(cs, /*step_params=*/true);
       crit = nullptr;
-      CAPGEN_HIP(hipEventRecord(ev_out, cs));
-      CAPGEN_HIP(hipStreamWaitEvent(es, ev_out, 0));
+      hz::record(ev_out, cs);
+      hz::wait(es, ev_out);
       return;
     }
     enter(cs);
@@ -1492,7 +1540,7 @@ struct capgen_engine {
     // under DP the forward graph holds the count and partial-CE all-reduces (RCCL ops capture);
     // a host-set global count (capgen_dp_set_global_count) runs the forward eagerly instead --
     // its pinned-memory copy must stay ordered against the host write
-    if (!graph_on && fwd_graph_on && !count_override) {
+    if (!graph_on && fwd_graph && !count_override) {
       // forward replayed as one linear hipGraph (cheap to launch: ~0.1 us/node of host time vs
       // ~2.7 us per eager launch, tools/kprobe.hip); backward issued eagerly on three streams
       // (a multi-branch graph costs the same host time per node as eager issue on ROCm 7)
@@ -1501,7 +1549,7 @@ struct capgen_engine {
         if (!tuned(B, N, T)) {  // autotune every GEMM shape outside the capture
           forward(f, ft, pos, caps, B, N, T, loss, /*drop_on=*/false, es);
           backward(es);
-          CAPGEN_HIP(hipStreamSynchronize(es));
+          hz::host_sync(es);
           tuned_shapes.push_back({B, N, T});
         }
         hipGraph_t graph = nullptr;
@@ -1561,7 +1609,7 @@ struct capgen_engine {
         if (!tuned(B, N, T)) {
           forward(f, ft, pos, caps, B, N, T, loss, /*drop_on=*/false, es);  // no RNG advance
           backward(es);
-          CAPGEN_HIP(hipStreamSynchronize(es));
+          hz::host_sync(es);
           tuned_shapes.push_back({B, N, T});
         }
         hipGraph_t graph = nullptr;
@@ -1704,7 +1752,7 @@ struct capgen_engine {
     if (gws && R <= g.R && N <= g.N) return;
     int nR = std::max(R, g.R), nN = std::max(N, g.N);
     if (gws) {
-      CAPGEN_HIP(hipStreamSynchronize(es));
+      hz::host_sync(es);
       CAPGEN_HIP(hipFree(gws));
       gws = nullptr;
       drop_gen_graph();
@@ -1723,7 +1771,7 @@ struct capgen_engine {
   void dec_step(int R, int Bimg, int N, int t, void* cache, const int32_t* ids, bool want_attn, hipStream_t s,
                 const int32_t* kv_row = nullptr) {
     const int dd = L.dd, Hd = L.Hd, dkd = dd / Hd, Tc = L.maxlen;
-    embedding_gather(P(L.emb), ids + t, Tc, R, L.dwe, g.E, act, s);
+    embedding_gather(P(L.emb), ids + t, Tc, R, L.dwe, g.E, act, s, L.V);
     linear(g.E, L.dwe, L.Wel, L.dwe, g.tmp, dd, act, R, dd, L.dwe, nullptr, 0, s);
     LnFwd ln;
     ln.M = R, ln.d = dd, ln.a = g.tmp, ln.pe = pe + (int64_t)t * dd, ln.pe_L = 1, ln.gamma = P(L.dec_lng);
@@ -2004,7 +2052,7 @@ int capgen_create(const capgen_config* cfg, int device, capgen_t** out) {
     CAPGEN_HIP(hipMalloc(&h->gstripe, (size_t)capgen_engine::NSTRIPE * h->n_small * sizeof(float)));
     CAPGEN_HIP(hipHostMalloc(&h->count_host, 64, hipHostMallocDefault));
     // the null-stream memsets above are not ordered before the engine's non-blocking streams
-    CAPGEN_HIP(hipDeviceSynchronize());
+    hz::host_sync(nullptr);
     *out = h.release();
   });
 }
@@ -2021,7 +2069,7 @@ int capgen_get_params(capgen_t* h, float* dst, int64_t n) {
   return guarded([&] {
     set_device(h);
     require(n == h->L.total, "get_params: size mismatch");
-    CAPGEN_HIP(hipStreamSynchronize(h->es));
+    hz::host_sync(h->es);
     CAPGEN_HIP(hipMemcpy(dst, h->params, n * 4, hipMemcpyDeviceToHost));
   });
 }
@@ -2030,10 +2078,10 @@ int capgen_set_params(capgen_t* h, const float* src, int64_t n) {
   return guarded([&] {
     set_device(h);
     require(n == h->L.total, "set_params: size mismatch");
-    CAPGEN_HIP(hipStreamSynchronize(h->es));
+    hz::host_sync(h->es);
     CAPGEN_HIP(hipMemcpy(h->params, src, n * 4, hipMemcpyHostToDevice));
     h->refresh_shadow(h->es);
-    CAPGEN_HIP(hipStreamSynchronize(h->es));
+    hz::host_sync(h->es);
   });
 }
 
@@ -2041,7 +2089,9 @@ int capgen_get_grads(capgen_t* h, float* dst, int64_t n) {
   return guarded([&] {
     set_device(h);
     require(n == h->L.total, "get_grads: size mismatch");
-    CAPGEN_HIP(hipStreamSynchronize(h->es));
+    require(!h->grads_sharded, "get_grads: after a sharded (ZeRO-1) step the gradient arena holds this rank's "
+                               "reduce-scattered chunks only (CAPGEN_ZERO=0 keeps whole gradients)");
+    hz::host_sync(h->es);
     CAPGEN_HIP(hipMemcpy(dst, h->grads, n * 4, hipMemcpyDeviceToHost));
   });
 }
@@ -2050,7 +2100,7 @@ int capgen_set_grads(capgen_t* h, const float* src, int64_t n) {
   return guarded([&] {
     set_device(h);
     require(n == h->L.total, "set_grads: size mismatch");
-    CAPGEN_HIP(hipStreamSynchronize(h->es));
+    hz::host_sync(h->es);
     CAPGEN_HIP(hipMemcpy(h->grads, src, n * 4, hipMemcpyHostToDevice));
   });
 }
@@ -2059,7 +2109,9 @@ int capgen_get_adam_state(capgen_t* h, int64_t* step, float* m, float* v, int64_
   return guarded([&] {
     set_device(h);
     require(n == h->L.total, "get_adam_state: size mismatch");
-    CAPGEN_HIP(hipStreamSynchronize(h->es));
+    require(!h->moments_sharded, "get_adam_state: the moments are sharded across ranks (ZeRO-1): call "
+                                 "capgen_dp_sync_adam_state on every rank first");
+    hz::host_sync(h->es);
     if (step) CAPGEN_HIP(hipMemcpy(step, h->step, 8, hipMemcpyDeviceToHost));
     if (m) CAPGEN_HIP(hipMemcpy(m, h->am, n * 4, hipMemcpyDeviceToHost));
     if (v) CAPGEN_HIP(hipMemcpy(v, h->av, n * 4, hipMemcpyDeviceToHost));
@@ -2070,13 +2122,13 @@ int capgen_set_adam_state(capgen_t* h, int64_t step, const float* m, const float
   return guarded([&] {
     set_device(h);
     require(n == h->L.total, "set_adam_state: size mismatch");
-    CAPGEN_HIP(hipStreamSynchronize(h->es));
+    hz::host_sync(h->es);
     CAPGEN_HIP(hipMemcpy(h->step, &step, 8, hipMemcpyHostToDevice));
     if (m) CAPGEN_HIP(hipMemcpy(h->am, m, n * 4, hipMemcpyHostToDevice));
     else CAPGEN_HIP(hipMemset(h->am, 0, n * 4));
     if (v) CAPGEN_HIP(hipMemcpy(h->av, v, n * 4, hipMemcpyHostToDevice));
     else CAPGEN_HIP(hipMemset(h->av, 0, n * 4));
-    CAPGEN_HIP(hipDeviceSynchronize());
+    hz::host_sync(nullptr);
   });
 }
 
@@ -2199,7 +2251,7 @@ int capgen_beam(capgen_t* h, const void* feats, int ft, const float* pos, int B,
 int capgen_set_rng_seed(capgen_t* h, uint64_t sd) {
   return guarded([&] {
     set_device(h);
-    CAPGEN_HIP(hipStreamSynchronize(h->es));
+    hz::host_sync(h->es);
     CAPGEN_HIP(hipMemcpy(h->seed, &sd, 8, hipMemcpyHostToDevice));
   });
 }
@@ -2293,7 +2345,7 @@ int capgen_debug_copy_buffer(capgen_t* h, int which, void* host_dst, int64_t byt
               : which == 6 ? h->a.genc[Le - 1].gA1 : which == 7 ? h->a.genc[Le - 1].gQKV
               : which >= 8 && which < 13 ? h->dbg_snap[which - 8] : nullptr;
     require(src != nullptr, "debug_copy_buffer: which in 0..12 (8-12 need CAPGEN_DEBUG_BWD_STOP=4)");
-    CAPGEN_HIP(hipDeviceSynchronize());
+    hz::host_sync(nullptr);
     CAPGEN_HIP(hipMemcpy(host_dst, src, (size_t)bytes, hipMemcpyDeviceToHost));
   });
 }
@@ -2307,6 +2359,66 @@ int capgen_debug_splitk_protocol(int proto) {
     require(proto >= 0 && proto < 1024, "debug_splitk_protocol: bits 0..9 only");
     gemm_set_splitk_protocol(proto);
   });
+}
+
+int capgen_tune_load(const char* path) {
+  int n = -1;
+  const int rc = guarded([&] {
+    require(path != nullptr, "tune_load: null path");
+    n = gemm_tune_load(path);
+  });
+  return rc ? -2 : n;
+}
+int capgen_tune_save(const char* path) {
+  int n = -1;
+  const int rc = guarded([&] {
+    require(path != nullptr, "tune_save: null path");
+    n = gemm_tune_save(path);
+    require(n >= 0, std::string("tune_save: cannot write ") + path);
+  });
+  return rc ? -2 : n;
+}
+int capgen_tune_live_count(void) { return gemm_tune_live_count(); }
+
+int capgen_debug_hazard(int op, char* report, int cap, int* n_conflicts) {
+  return guarded([&] {
+    require(op >= 0 && op <= 2, "debug_hazard: op 0 (off), 1 (on + clear) or 2 (check)");
+    if (op == 0) return hz::enable(false);
+    if (op == 1) {
+      hz::reset();
+      return hz::enable(true);
+    }
+    std::string rep;
+    const int n = hz::check(&rep);
+    if (n_conflicts) *n_conflicts = n;
+    if (report && cap > 0) {
+      const size_t k = std::min<size_t>(rep.size(), (size_t)cap - 1);
+      std::memcpy(report, rep.data(), k);
+      report[k] = 0;
+    }
+  });
+}
+int capgen_debug_collectives(capgen_t* h, int op, char* out, int cap) {
+  return guarded([&] {
+    require(h != nullptr, "null engine handle");
+    require(op >= 0 && op <= 2, "debug_collectives: op 0 (off), 1 (on + clear) or 2 (dump)");
+    if (op < 2) {
+      h->coll_log_on = op == 1;
+      h->coll_log.clear();
+      return;
+    }
+    std::string all;
+    for (auto& l : h->coll_log) all += l + "\n";
+    if (out && cap > 0) {
+      const size_t k = std::min<size_t>(all.size(), (size_t)cap - 1);
+      std::memcpy(out, all.data(), k);
+      out[k] = 0;
+    }
+  });
+}
+
+int capgen_debug_side_delay(double us) {
+  return guarded([&] { hz::set_delay_us(us); });
 }
 
 int capgen_dp_unique_id(char out[128]) {
@@ -2330,15 +2442,15 @@ int capgen_dp_init(capgen_t* h, const char id[128], int rank, int world) {
     // replicate rank 0's parameters
     NCCL_CHECK(ncclBroadcast(h->params, h->params, (size_t)h->L.total, ncclFloat, 0, h->comm, h->es));
     h->refresh_shadow(h->es);
-    CAPGEN_HIP(hipStreamSynchronize(h->es));
+    hz::host_sync(h->es);
   });
 }
 
 int capgen_dp_sync_adam_state(capgen_t* h) {
   return guarded([&] {
     set_device(h);
-    CAPGEN_HIP(hipStreamSynchronize(h->es));
-    CAPGEN_HIP(hipStreamSynchronize(h->ec));
+    hz::host_sync(h->es);
+    hz::host_sync(h->ec);
     const int zw = h->zworld();
     if (!h->comm || zw <= 1 || !h->zsharded()) return;
     for (auto& b : h->zbuckets) {
@@ -2347,7 +2459,8 @@ int capgen_dp_sync_adam_state(capgen_t* h) {
       NCCL_CHECK(ncclAllGather(h->am + o, h->am + b[0], (size_t)c, ncclFloat, h->comm, h->es));
       NCCL_CHECK(ncclAllGather(h->av + o, h->av + b[0], (size_t)c, ncclFloat, h->comm, h->es));
     }
-    CAPGEN_HIP(hipStreamSynchronize(h->es));
+    h->moments_sharded = false;
+    hz::host_sync(h->es);
   });
 }
 

@@ -68,4 +68,12 @@ void gemm_grouped(const GemmArgs* probs, int n, DType out, bool ta, bool tb, hip
 // bf16-operand path (gemm_bf16.hip); called by gemm() after argument checks
 void gemm_bf16(const GemmArgs& g, DType out, bool ta, bool tb, hipStream_t s);
 
+// Persisted autotune table (gemm_bf16.hip): one line per tuned shape / grouped signature.
+// load: merges the file's choices (entries already tuned in this process win); returns the
+// number of entries read (-1: no such file).  save: writes every choice made or loaded so far.
+int gemm_tune_load(const char* path);
+int gemm_tune_save(const char* path);
+// number of GEMM shapes autotuned live in this process (a complete table keeps it at 0)
+int gemm_tune_live_count();
+
 }  // namespace capgen

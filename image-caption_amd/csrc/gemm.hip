@@ -15,7 +15,9 @@
 // transposed on the LDS write so every MFMA fragment is one 16-B ds_read (bf16).
 #include <chrono>
 #include <cstdio>
+#include <vector>
 #include "gemm.h"
+#include "hazard.h"
 #include "ops.h"
 
 namespace capgen {
@@ -212,6 +214,26 @@ static void launch_layout(const GemmArgs& g, bool ta, bool tb, hipStream_t s) {
   else launch_tiles<T, TO, true, true>(g, s);
 }
 
+// the device bytes one GEMM touches (hazard checker, hazard.h; also used by gemm_grouped)
+void gemm_hz_regions(const GemmArgs& g, DType in, DType out, bool ta, bool tb, std::vector<hz::Rgn>& v) {
+  using namespace hz;
+  const int64_t ei = dsize(in), eo = dsize(out);
+  const int ncol = g.C2 ? g.nsplit : g.N;
+  v.push_back(ta ? blk(g.A, g.K, g.M * ei, g.lda * ei, RD) : blk(g.A, g.M, g.K * ei, g.lda * ei, RD));
+  v.push_back(tb ? blk(g.B, g.K, g.N * ei, g.ldb * ei, RD) : blk(g.B, g.N, g.K * ei, g.ldb * ei, RD));
+  v.push_back(blk(g.C, g.M, ncol * eo, g.ldc * eo, WR));
+  if (g.beta) v.push_back(blk(g.C, g.M, ncol * eo, g.ldc * eo, RD));
+  if (g.C2) v.push_back(blk(g.C2, g.M, (int64_t)(g.N - g.nsplit) * eo, g.ldc2 * eo, WR));
+  v.push_back(blk(g.aux, g.M, g.N * ei, g.ldaux * ei, RD));
+  v.push_back(blk(g.cin, g.M, g.N * 4, g.ldcin * 4, RD));
+  v.push_back(rd(g.bias, g.N * 4));
+  v.push_back(rd(g.alpha_ptr, 4));
+  v.push_back(blk(g.colsum, g.colsum_stripes, g.N * 4, g.colsum_stride * 4, ACC));
+  v.push_back(blk(g.ce_stats, g.M, (int64_t)((g.N + 15) / 16) * 8, g.ce_ld * 8, WR));
+  v.push_back(rd(g.ce_tgt, (int64_t)g.M * 4));
+  v.push_back(wr(g.ce_tlogit, (int64_t)g.M * 4));
+}
+
 static void gemm_impl(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t s);
 // CAPGEN_HOST_TIMING (diagnostic): average host time of a gemm() call, printed every 2000 calls
 void gemm(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t s) {
@@ -241,6 +263,11 @@ static void gemm_impl(const GemmArgs& g, DType in, DType out, bool ta, bool tb, 
   require(!g.cin || in == DType::BF16, "gemm: cin is a bf16-path epilogue input");
   require(!g.C2 || (in == DType::BF16 && g.nsplit % 4 == 0 && !g.beta && !g.colsum),
           "gemm: a split output (C2) needs the bf16 path, nsplit % 4 == 0, no beta / colsum");
+  if (hz::active()) {
+    std::vector<hz::Rgn> v;
+    gemm_hz_regions(g, in, out, ta, tb, v);
+    hz::op(s, ta ? "gemm TN (dW)" : tb ? "gemm NN (dX)" : "gemm NT (fwd)", v.data(), v.size());
+  }
   if (in == DType::F32) {
     if (out == DType::F32) launch_layout<float, float>(g, ta, tb, s);
     else launch_layout<float, bf16>(g, ta, tb, s);

@@ -29,6 +29,8 @@
 // an A row-panel) land on the same XCD L2.
 #include <chrono>
 #include <algorithm>
+#include <dlfcn.h>
+#include <string>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -38,8 +40,11 @@
 #include <vector>
 
 #include "gemm.h"
+#include "hazard.h"
 
 namespace capgen {
+
+void gemm_hz_regions(const GemmArgs& g, DType in, DType out, bool ta, bool tb, std::vector<hz::Rgn>& v);  // gemm.hip
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
@@ -701,6 +706,7 @@ struct Choice {
 };
 std::map<TuneKey, Choice> g_tuned;
 std::mutex g_tune_mu;
+int g_live_tuned = 0;  // shapes (plain + grouped) tuned live in this process
 
 bool autotune_enabled() {
   static const bool on = [] {
@@ -881,16 +887,22 @@ static void launch_bf16_tiles(const GemmArgs& g, hipStream_t s) {
   if (c.splitk > 1) ensure_ws(s, splitk_bytes(g, c.splitk));
   if (c.variant == 0) {
     c.variant = heuristic_variant(g);
-    if (autotune_enabled()) {
-      TuneKey key{g.M, g.N, g.K, TA, TB, (int)sizeof(TO)};
-      std::lock_guard<std::mutex> lk(g_tune_mu);
-      auto it = g_tuned.find(key);
-      if (it != g_tuned.end()) {
-        c = it->second;
-      } else {
-        hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-        CAPGEN_HIP(hipStreamIsCapturing(s, &st));
-        if (st == hipStreamCaptureStatusNone) c = g_tuned[key] = tune<TO, TA, TB>(g, s);
+    TuneKey key{g.M, g.N, g.K, TA, TB, (int)sizeof(TO)};
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    auto it = g_tuned.find(key);  // tuned in this process or loaded from the persisted table
+    if (it != g_tuned.end()) {
+      c = it->second;
+    } else if (autotune_enabled()) {
+      hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+      CAPGEN_HIP(hipStreamIsCapturing(s, &st));
+      if (st == hipStreamCaptureStatusNone) {
+        // a shape the table does not hold: tune it on an idle device (every stream drained, so
+        // no concurrent kernel shares the CUs or the caches with the candidates' clock, and the
+        // candidates run strictly between the work issued before and after this call)
+        CAPGEN_HIP(hipDeviceSynchronize());
+        c = g_tuned[key] = tune<TO, TA, TB>(g, s);
+        CAPGEN_HIP(hipStreamSynchronize(s));
+        ++g_live_tuned;
       }
     }
   }
@@ -987,6 +999,8 @@ static void launch_group(const GemmArgs* ps, int n, hipStream_t s) {
       hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
       CAPGEN_HIP(hipStreamIsCapturing(s, &st));
       if (st == hipStreamCaptureStatusNone && autotune_enabled()) {
+        CAPGEN_HIP(hipDeviceSynchronize());  // idle device (see launch_bf16_tiles)
+        ++g_live_tuned;
         // time each variant on scratch outputs (inputs untouched, beta forced to 0)
         std::vector<GemmArgs> t(ps, ps + n);
         std::vector<void*> scratch(n);
@@ -1006,6 +1020,7 @@ static void launch_group(const GemmArgs* ps, int n, hipStream_t s) {
         CAPGEN_HIP(hipEventDestroy(e0));
         CAPGEN_HIP(hipEventDestroy(e1));
         for (void* p : scratch) CAPGEN_HIP(hipFree(p));
+        CAPGEN_HIP(hipStreamSynchronize(s));
         g_group_tuned[key] = v;
         if (std::getenv("CAPGEN_AUTOTUNE_LOG"))
           std::fprintf(stderr, "[capgen gemm] group of %d (M=%d N=%d K=%d first) -> %s (%.2f us)\n", n, ps[0].M,
@@ -1042,6 +1057,11 @@ static void gemm_grouped_impl(const GemmArgs* ps, int n, DType out, bool ta, boo
             "gemm_grouped: bad problem shape");
     require(((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0, "gemm_grouped: operands must be 16-B aligned");
   }
+  if (hz::active()) {
+    std::vector<hz::Rgn> v;
+    for (int i = 0; i < n; ++i) gemm_hz_regions(ps[i], DType::BF16, out, ta, tb, v);
+    hz::op(s, "gemm grouped (dW)", v.data(), v.size());
+  }
   if (out == DType::F32) {
     if (ta && tb) launch_group<float, true, true>(ps, n, s);
     else if (!ta && tb) launch_group<float, false, true>(ps, n, s);
@@ -1054,6 +1074,69 @@ static void gemm_grouped_impl(const GemmArgs* ps, int n, DType out, bool ta, boo
   CAPGEN_HIP(hipGetLastError());
 }
 
+// ---- persisted autotune table --------------------------------------------------------------
+// Text, one choice per line:  g M N K ta tb out_bytes variant splitk
+//                             G ta tb out_bytes n M1 N1 K1 ... Mn Nn Kn variant
+int gemm_tune_load(const char* path) {
+  FILE* f = std::fopen(path, "r");
+  if (!f) return -1;
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  int n = 0;
+  char line[1024];
+  while (std::fgets(line, sizeof line, f)) {
+    if (line[0] == 'g') {
+      TuneKey k{};
+      Choice c{};
+      if (std::sscanf(line + 1, "%d %d %d %d %d %d %d %d", &k.M, &k.N, &k.K, &k.ta, &k.tb, &k.out, &c.variant,
+                      &c.splitk) == 8 &&
+          c.variant >= 1 && c.variant <= NVARIANTS && c.splitk >= 1 && c.splitk <= 16) {
+        g_tuned.emplace(k, c);
+        ++n;
+      }
+    } else if (line[0] == 'G') {
+      std::vector<int> v;
+      const char* p = line + 1;
+      int x, used = 0;
+      while (std::sscanf(p, "%d%n", &x, &used) == 1) v.push_back(x), p += used;
+      if (v.size() >= 5 && v.size() == 4 + 3 * (size_t)v[3] + 1) {
+        const int var = v.back();
+        std::vector<int> key{v[0], v[1], v[2]};
+        key.insert(key.end(), v.begin() + 4, v.end() - 1);
+        g_group_tuned.emplace(key, var);
+        ++n;
+      }
+    }
+  }
+  std::fclose(f);
+  return n;
+}
+
+int gemm_tune_save(const char* path) {
+  FILE* f = std::fopen(path, "w");
+  if (!f) return -1;
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  std::fprintf(f, "# capgen bf16 GEMM autotune table (gfx950): g M N K ta tb out_bytes variant splitk | "
+                  "G ta tb out_bytes n (M N K)xn variant\n");
+  int n = 0;
+  for (auto& kv : g_tuned) {
+    const TuneKey& k = kv.first;
+    std::fprintf(f, "g %d %d %d %d %d %d %d %d  # %s\n", k.M, k.N, k.K, k.ta, k.tb, k.out, kv.second.variant,
+                 kv.second.splitk, kVariantName[kv.second.variant]);
+    ++n;
+  }
+  for (auto& kv : g_group_tuned) {
+    const std::vector<int>& k = kv.first;
+    std::fprintf(f, "G %d %d %d %d", k[0], k[1], k[2], (int)(k.size() - 3) / 3);
+    for (size_t i = 3; i < k.size(); ++i) std::fprintf(f, " %d", k[i]);
+    std::fprintf(f, " %d  # %s\n", kv.second, kVariantName[kv.second]);
+    ++n;
+  }
+  std::fclose(f);
+  return n;
+}
+
+int gemm_tune_live_count() { return g_live_tuned; }
+
 void gemm_set_variant(int v) { g_variant = v; }
 void gemm_set_splitk_protocol(int p) { g_splitk_proto = p; }
 void gemm_splitk_diag(int* out4, bool reset) {
@@ -1065,7 +1148,30 @@ void gemm_splitk_diag(int* out4, bool reset) {
   }
 }
 
+// the persisted autotune table: $CAPGEN_TUNE_TABLE, else tune_gfx950.txt next to libcapgen.so
+// ("0" or "": none), loaded once per process before the first GEMM
+static void load_default_tune_table() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    const char* e = std::getenv("CAPGEN_TUNE_TABLE");
+    std::string path;
+    if (e) {
+      if (!e[0] || (e[0] == '0' && !e[1])) return;
+      path = e;
+    } else {
+      Dl_info info;
+      if (!dladdr((void*)&gemm_init, &info) || !info.dli_fname) return;
+      path = info.dli_fname;
+      const size_t slash = path.rfind('/');
+      path = (slash == std::string::npos ? std::string(".") : path.substr(0, slash)) + "/tune_gfx950.txt";
+    }
+    const int n = gemm_tune_load(path.c_str());
+    if (std::getenv("CAPGEN_AUTOTUNE_LOG")) std::fprintf(stderr, "[capgen gemm] tune table %s: %d entries\n", path.c_str(), n);
+  });
+}
+
 void gemm_init() {
+  load_default_tune_table();
   int dev = 0;
   CAPGEN_HIP(hipGetDevice(&dev));
   require(dev >= 0 && dev < 64, "gemm_init: device index out of range");

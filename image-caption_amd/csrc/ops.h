@@ -62,11 +62,12 @@ void pack_encoder_input(const void* feats, DType feats_t, const float* pos, int 
 void prepare_captions(const int32_t* caps, int B, int T, int pad, int32_t* ids_in, int32_t* tgt,
                       float* count, hipStream_t s, uint64_t* seed_bump = nullptr);
 // out[m] = table[ids[m]] (f32 table -> T)                                      (model.py:432)
+// (table_rows: rows of the table, for the hazard checker's byte ranges only)
 void embedding_gather(const float* table, const int32_t* ids, int64_t ids_ld, int M, int d, void* out, DType t,
-                      hipStream_t s);
+                      hipStream_t s, int64_t table_rows = 0);
 // grad[ids[m]] += dE[m] for ids[m] != pad  (nn.Embedding padding_idx)
 void embedding_scatter_add(const void* dE, const int32_t* ids, int M, int d, int pad, float* grad, DType t,
-                           hipStream_t s);
+                           hipStream_t s, int64_t table_rows = 0);
 // db[n] += alpha (* *alpha_ptr) * sum_m X[m][n]
 void column_sum(const void* X, int M, int N, int64_t ldx, float alpha, const float* alpha_ptr, float* db,
                 DType t, hipStream_t s, int stripes = 1, int64_t stripe_stride = 0);

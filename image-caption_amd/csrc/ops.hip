@@ -9,6 +9,7 @@
 #include <cstdlib>
 
 #include "ops.h"
+#include "hazard.h"
 
 namespace capgen {
 
@@ -240,6 +241,13 @@ static void ln_sums_dispatch(const LnBwd& a, hipStream_t s) {
 void layernorm_param_sums(const LnBwd& a, DType t, hipStream_t s) {
   if (a.M <= 0 || (skip_mask() & 128) || (!a.dgamma && !a.dbias)) return;
   require(a.dy && a.v && a.mean && a.rstd && (!a.dbias || a.d_a), "layernorm_param_sums: missing inputs");
+  if (hz::active()) {
+    using namespace hz;
+    const int64_t row = a.d * (int64_t)dsize(t), sb = a.d * 4, ss = std::max<int64_t>(a.stripe_stride * 4, sb);
+    op(s, "ln_param_sums", {rd(a.dy, a.M * row), rd(a.v, a.M * row), rd(a.mean, a.M * 4), rd(a.rstd, a.M * 4),
+                            rd(a.d_a, a.M * row), blk(a.dgamma, a.stripes, sb, ss, ACC), blk(a.dbeta, a.stripes, sb, ss, ACC),
+                            blk(a.dbias, a.stripes, sb, ss, ACC)});
+  }
   if (t == DType::F32) ln_sums_dispatch<float>(a, s);
   else ln_sums_dispatch<bf16>(a, s);
   CAPGEN_HIP(hipGetLastError());
@@ -259,6 +267,14 @@ static void ln_fwd_dispatch(const LnFwd& a, hipStream_t s) {
 }
 void layernorm_fwd(const LnFwd& a, DType t, hipStream_t s) {
   if (a.M <= 0 || (skip_mask() & 1)) return;
+  if (hz::active()) {
+    using namespace hz;
+    const int64_t row = a.d * (int64_t)dsize(t);
+    op(s, "ln_fwd", {rd(a.a, a.M * row), rd(a.a_bias, a.d * 4), rd(a.res, a.M * row), rd(a.pe, (int64_t)a.pe_L * a.d * 4),
+                     rd(a.gamma, a.d * 4), rd(a.beta, a.d * 4), blk(a.mask.ids, a.M, 4, a.mask.ids_ld * 4, RD),
+                     rd(a.mask.valid, a.M), rd(a.drop.seed_ptr, 8), wr(a.y, a.M * row), wr(a.v_save, a.M * row),
+                     wr(a.mean, a.M * 4), wr(a.rstd, a.M * 4)});
+  }
   if (t == DType::F32) ln_fwd_dispatch<float>(a, s);
   else ln_fwd_dispatch<bf16>(a, s);
   CAPGEN_HIP(hipGetLastError());
@@ -296,6 +312,15 @@ static void ln_bwd_dispatch(const LnBwd& a, hipStream_t s) {
 void layernorm_bwd(const LnBwd& a_in, DType t, hipStream_t s) {
   if (a_in.M <= 0 || (skip_mask() & 4)) return;
   LnBwd a = a_in;
+  if (hz::active()) {
+    using namespace hz;
+    const int64_t row = a.d * (int64_t)dsize(t), sb = a.d * 4, ss = std::max<int64_t>(a.stripe_stride * 4, sb);
+    op(s, "ln_bwd", {rd(a.dy, a.M * row), rd(a.v, a.M * row), rd(a.mean, a.M * 4), rd(a.rstd, a.M * 4),
+                     rd(a.gamma, a.d * 4), blk(a.mask.ids, a.M, 4, a.mask.ids_ld * 4, RD), rd(a.mask.valid, a.M),
+                     rd(a.drop.seed_ptr, 8), wr(a.d_res, a.M * row), wr(a.d_a, a.M * row), wr(a.y_save, a.M * row),
+                     blk(a.dgamma, a.stripes, sb, ss, ACC), blk(a.dbeta, a.stripes, sb, ss, ACC),
+                     blk(a.dbias, a.stripes, sb, ss, ACC)});
+  }
   if (skip_mask() & 128) a.dgamma = a.dbeta = a.dbias = nullptr;  // diagnostic: no parameter-gradient sums
   if (t == DType::F32) ln_bwd_dispatch<float>(a, s);
   else ln_bwd_dispatch<bf16>(a, s);
@@ -357,6 +382,12 @@ void pack_encoder_input(const void* feats, DType ft, const float* pos, int M, in
   if (M <= 0) return;
   require(F % 8 == 0 && ((uintptr_t)feats & 15) == 0, "pack: feature width must be a multiple of 8, 16-B aligned");
   require(img_idx == nullptr || N > 0, "pack: indexed gather needs N");
+  if (hz::active()) {
+    using namespace hz;
+    const int64_t src_rows = img_idx ? (int64_t)n_img * N : M;
+    op(s, "pack", {rd(feats, src_rows * F * (int64_t)dsize(ft)), rd(pos, src_rows * P * 4), rd(img_idx, img_idx ? M / N * 4 : 0),
+                   wr(out, (int64_t)M * Kp * dsize(ot)), wr(valid, M), wr(seed_bump, 8)});
+  }
   dim3 grid(M);
   if (ft == DType::F32 && ot == DType::F32)
     pack_kernel<float, float><<<grid, 256, 0, s>>>((const float*)feats, pos, img_idx, n_img, N, F, P, Kp, (float*)out, valid, seed_bump);
@@ -392,6 +423,11 @@ __global__ void prep_caps_kernel(const int32_t* __restrict__ caps, int B, int T,
 
 void prepare_captions(const int32_t* caps, int B, int T, int pad, int32_t* ids_in, int32_t* tgt, float* count,
                       hipStream_t s, uint64_t* seed_bump) {
+  if (hz::active()) {
+    using namespace hz;
+    op(s, "prep_captions", {rd(caps, (int64_t)B * T * 4), wr(ids_in, (int64_t)B * (T - 1) * 4),
+                            wr(tgt, (int64_t)B * (T - 1) * 4), wr(count, 4), wr(seed_bump, 8)});
+  }
   prep_caps_kernel<<<1, 1024, 0, s>>>(caps, B, T, pad, ids_in, tgt, count, seed_bump);
   CAPGEN_HIP(hipGetLastError());
 }
@@ -407,8 +443,11 @@ __global__ void gather_kernel(const float* __restrict__ table, const int32_t* __
   }
 }
 void embedding_gather(const float* table, const int32_t* ids, int64_t ids_ld, int M, int d, void* out, DType t,
-                      hipStream_t s) {
+                      hipStream_t s, int64_t table_rows) {
   if (M <= 0) return;
+  if (hz::active())
+    hz::op(s, "emb_gather", {hz::rd(table, table_rows * d * 4), hz::blk(ids, M, 4, ids_ld * 4, hz::RD),
+                             hz::wr(out, (int64_t)M * d * dsize(t))});
   int64_t n = (int64_t)M * d;
   int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
   if (t == DType::F32) gather_kernel<float><<<grid, 256, 0, s>>>(table, ids, ids_ld, M, d, (float*)out);
@@ -428,8 +467,11 @@ __global__ void scatter_kernel(const T* __restrict__ dE, const int32_t* __restri
   }
 }
 void embedding_scatter_add(const void* dE, const int32_t* ids, int M, int d, int pad, float* grad, DType t,
-                           hipStream_t s) {
+                           hipStream_t s, int64_t table_rows) {
   if (M <= 0) return;
+  if (hz::active())
+    hz::op(s, "emb_scatter", {hz::rd(dE, (int64_t)M * d * dsize(t)), hz::rd(ids, (int64_t)M * 4),
+                              hz::acc(grad, table_rows * d * 4)});
   int64_t n = (int64_t)M * d;
   int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
   if (t == DType::F32) scatter_kernel<float><<<grid, 256, 0, s>>>((const float*)dE, ids, M, d, pad, grad);
@@ -482,6 +524,11 @@ void column_sum(const void* X, int M, int N, int64_t ldx, float alpha, const flo
   if (M <= 0 || N <= 0) return;
   const int V = t == DType::F32 ? 4 : 8;
   require(N % V == 0 && ldx % V == 0, "column_sum: N/ld must be multiples of 16 B");
+  if (hz::active()) {
+    using namespace hz;
+    op(s, "column_sum", {blk(X, M, N * (int64_t)dsize(t), ldx * (int64_t)dsize(t), RD), rd(alpha_ptr, 4),
+                         blk(db, stripes, N * 4, std::max<int64_t>(stripe_stride * 4, N * 4), ACC)});
+  }
   dim3 grid((N + 8 * V - 1) / (8 * V), (M + 255) / 256);
   if (t == DType::F32) colsum_kernel<float><<<grid, 256, 0, s>>>((const float*)X, M, N, ldx, alpha, alpha_ptr, db, stripes,
                                                                stripe_stride);
@@ -503,6 +550,12 @@ __global__ void stripe_reduce_kernel(float* __restrict__ S, int stripes, int64_t
 void stripe_reduce(float* S, int stripes, int64_t stride, int64_t n, float* dst, int accumulate, hipStream_t s,
                    int clear) {
   if (n <= 0) return;
+  if (hz::active()) {
+    using namespace hz;
+    const int64_t ss = std::max<int64_t>(stride * 4, n * 4);
+    op(s, "stripe_reduce", {blk(S, stripes, n * 4, ss, clear ? WR : RD), blk(S, stripes, n * 4, ss, RD), wr(dst, n * 4),
+                            accumulate ? rd(dst, n * 4) : Rgn{}});
+  }
   int grid = (int)std::min<int64_t>((n + 255) / 256, 1024);
   stripe_reduce_kernel<<<grid, 256, 0, s>>>(S, stripes, stride, n, dst, accumulate, clear);
   CAPGEN_HIP(hipGetLastError());
@@ -614,6 +667,9 @@ static void ce_launch(const float* logits, const int32_t* tgt, int M, int V, int
 void cross_entropy_rows(const float* logits, const int32_t* tgt, int M, int V, int pad, float* loss_row, void* dl,
                         DType t, hipStream_t s) {
   if (M <= 0) return;
+  if (hz::active())
+    hz::op(s, "cross_entropy", {hz::rd(logits, (int64_t)M * V * 4), hz::rd(tgt, (int64_t)M * 4),
+                                hz::wr(loss_row, (int64_t)M * 4), hz::wr(dl, (int64_t)M * V * dsize(t))});
   if (t == DType::F32) ce_launch<float>(logits, tgt, M, V, pad, loss_row, (float*)dl, s);
   else ce_launch<bf16>(logits, tgt, M, V, pad, loss_row, (bf16*)dl, s);
   CAPGEN_HIP(hipGetLastError());
@@ -681,6 +737,11 @@ void ce_finish(const float2* stats, int64_t ld, const float* tlogit, const int32
                float* loss_row, bf16* dl, hipStream_t s) {
   if (M <= 0) return;
   require(V % 4 == 0 && ld >= (V + 15) / 16, "ce_finish: V must be a multiple of 4");
+  if (hz::active()) {
+    using namespace hz;
+    op(s, "ce_finish", {blk(stats, M, (int64_t)((V + 15) / 16) * 8, ld * 8, RD), rd(tlogit, (int64_t)M * 4),
+                        rd(tgt, (int64_t)M * 4), wr(loss_row, (int64_t)M * 4), wr(dl, (int64_t)M * V * 2)});
+  }
   const int spt = ((V + 15) / 16 + 255) / 256;
   if (spt <= 1) ce_finish_kernel<1><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl);
   else if (spt <= 2) ce_finish_kernel<2><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl);
@@ -720,6 +781,9 @@ __global__ void loss_finalize_kernel(const float* __restrict__ loss_row, int M, 
 }
 void loss_finalize(const float* loss_row, int M, const float* count, int focal, float* loss_out, float* grad_scale,
                    hipStream_t s, const float* ce_in, int partial) {
+  if (hz::active())
+    hz::op(s, "loss_finalize", {hz::rd(ce_in ? nullptr : loss_row, (int64_t)M * 4), hz::rd(count, 4), hz::rd(ce_in, 4),
+                                hz::wr(loss_out, 4), hz::wr(partial ? nullptr : grad_scale, 4)});
   loss_finalize_kernel<<<1, 256, 0, s>>>(loss_row, M, count, focal, ce_in, partial, loss_out, grad_scale);
   CAPGEN_HIP(hipGetLastError());
 }
@@ -733,6 +797,7 @@ __global__ void adam_prep_kernel(int64_t* step, float lr, float b1, float b2, fl
   scal[1] = (float)sqrt(bc2);            // bias_correction2_sqrt
 }
 void adam_prepare(int64_t* step, float lr, float b1, float b2, float* scal, hipStream_t s) {
+  if (hz::active()) hz::op(s, "adam_prepare", {hz::wr(step, 8), hz::wr(scal, 8)});
   adam_prep_kernel<<<1, 1, 0, s>>>(step, lr, b1, b2, scal);
   CAPGEN_HIP(hipGetLastError());
 }
@@ -764,6 +829,9 @@ void adam_update(float* p, const float* g, float* m, float* v, size_t n, float b
                  const float* scal, bf16* shadow, size_t n_shadow, hipStream_t s, int grid_cap) {
   require(n % 4 == 0 && n_shadow % 4 == 0, "adam: arena size must be a multiple of 4");
   if (skip_mask() & 32) return;
+  if (hz::active())
+    hz::op(s, "adam", {hz::rd(g, (int64_t)n * 4), hz::rd(scal, 8), hz::wr(p, (int64_t)n * 4), hz::wr(m, (int64_t)n * 4),
+                       hz::wr(v, (int64_t)n * 4), hz::wr(shadow, (int64_t)n_shadow * 2)});
   size_t n4 = n / 4;
   static const int cap = [] {  // Adam workgroups (grid-stride): one per CU leaves the other wave slots to the
     // critical stream (A/B over 4 runs each: 3.046 vs 3.070 ms/step with 8 per CU; CAPGEN_ADAM_GRID)
@@ -792,6 +860,7 @@ __global__ void to_bf16x4_kernel(const float4* __restrict__ src, bf16* __restric
 }
 void to_bf16(const float* src, bf16* dst, size_t n, hipStream_t s) {
   if (!n) return;
+  if (hz::active()) hz::op(s, "to_bf16", {hz::rd(src, (int64_t)n * 4), hz::wr(dst, (int64_t)n * 2)});
   if (n % 4 == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 7) == 0) {
     const size_t n4 = n / 4;
     int grid = (int)std::min<size_t>((n4 + 255) / 256, 2048);

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define CAPGEN_ABI_VERSION 5
+#define CAPGEN_ABI_VERSION 6
 
 typedef struct capgen_engine capgen_t;
 
@@ -205,6 +205,29 @@ int capgen_scst_rewards(const int64_t* target, int64_t target_ld, const int64_t*
 int capgen_debug_attention(int dtype, int B, int H, int Lq, int Lk, int dk, const void* q, const void* k,
                            const void* v, const unsigned char* key_valid, int causal, float temperature, void* o,
                            float* probs, const void* dout, void* dq, void* dk_, void* dv, void* stream);
+
+/* Persisted GEMM autotune table (no reference counterpart: the reference's GEMMs are cuBLAS calls
+ * of torch eager, models.py:120-126).  The bf16 GEMM picks a tile / wave / pipeline / split-K
+ * variant per shape by timing; a table file fixes those choices so that every process (bench,
+ * tests, profiles) runs the same kernels.  load merges a file (returns the entries read, or -1:
+ * no file); save writes every choice known to this process; tune_live_count = shapes this
+ * process had to tune itself (a complete table keeps it 0).  libcapgen loads
+ * $CAPGEN_TUNE_TABLE (default: tune_gfx950.txt next to the library) at first use. */
+int capgen_tune_load(const char* path);
+int capgen_tune_save(const char* path);
+int capgen_tune_live_count(void);
+
+/* Diagnostics of the multi-stream step (hazard.h): op 1 = start logging every launch's stream and
+ * device byte ranges and every event / host-sync edge (clears the log), 0 = stop, 2 = check the log:
+ * *n_conflicts = unordered pairs of launches on different streams touching overlapping bytes (at
+ * least one writing), report (cap bytes, NUL-terminated) = the first of them.  side_delay: a spin
+ * kernel of `us` microseconds in front of every launch off the critical stream (0 = off). */
+int capgen_debug_hazard(int op, char* report, int cap, int* n_conflicts);
+int capgen_debug_side_delay(double us);
+/* The engine's RCCL call sequence (op 1 = start recording + clear, 0 = stop, 2 = dump one line per
+ * collective: name, bytes, stream role).  Every rank must issue the identical sequence whatever its
+ * batch, or the ranks deadlock (test hook for the data-parallel step). */
+int capgen_debug_collectives(capgen_t* h, int op, char* out, int cap);
 
 /* Data parallel (one process per GPU, RCCL over xGMI).  Rank 0 creates the 128-byte
  * unique id; the host broadcasts it (torch.distributed store) and every rank calls

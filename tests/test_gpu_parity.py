@@ -162,7 +162,7 @@ def test_dp_world1_rccl_train_step_fp32(graph):
 @pytest.mark.parametrize("dp", [False, True])
 def test_split_forward_graphs_equal_eager_fp32(monkeypatch, dp):
     """The forward as split linear graphs (pre / decoder front on es2 / encoder / decoder, events
-    between them; CAPGEN_FWD_SPLIT=1, the default under DP with world > 1) equals the eager
+    between them; CAPGEN_FWD_SPLIT=1) equals the eager
     forward over three bucketed train steps, with and without the RCCL DP path (world 1)."""
     from capgen.engine import Engine
     cfg, seed, z = load_fixture("c2s")
