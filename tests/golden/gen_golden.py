@@ -307,6 +307,8 @@ RL_FIXTURES = {
     # tag: (cfg, B, N, T, seed, min_valid, pad_frac)
     "c5_rl": (preset("C1"), 8, 8, 10, 5, 4, 0.0),
     "c5_rl_pad": (preset("C1"), 8, 8, 10, 6, 4, 0.35),
+    # the C5 model itself (6+6 blocks, d=512, h=8, 36 regions, T=20) at the c2s vocabulary
+    "c5_rl_c2s": (preset("C2", num_vocab=1000), 4, 36, 20, 12, 12, 0.2),
 }
 
 

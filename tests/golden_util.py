@@ -23,6 +23,7 @@ FIXTURE_CFG = {
     # RL_FIXTURES (SCST, injected rewards)
     "c5_rl": (lambda: preset("C1"), 5),
     "c5_rl_pad": (lambda: preset("C1"), 6),
+    "c5_rl_c2s": (lambda: preset("C2", num_vocab=1000), 12),
 }
 
 

@@ -104,7 +104,7 @@ def rl_setup(tag):
     return cfg, sd, x, z, base
 
 
-@pytest.mark.parametrize("tag", ["c5_rl", "c5_rl_pad"])
+@pytest.mark.parametrize("tag", ["c5_rl", "c5_rl_pad", "c5_rl_c2s"])
 def test_rl_loss_and_grads(tag):
     """SelfCriticNetwork step mechanics (model_RL.py:75-97, loss.py:31-220) with injected rewards."""
     cfg, sd, (f, p, c), z, base = rl_setup(tag)
