@@ -92,6 +92,7 @@ _SIGS = {
     "capgen_debug_hazard": (C.c_int, [C.c_int, C.c_char_p, C.c_int, C.POINTER(C.c_int)]),
     "capgen_debug_side_delay": (C.c_int, [C.c_double]),
     "capgen_debug_collectives": (C.c_int, [_P, C.c_int, C.c_char_p, C.c_int]),
+    "capgen_debug_stamps": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_char_p, C.c_int]),
     "capgen_scst_rewards": (C.c_int, [_P, C.c_int64, _P, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                       C.c_int64, C.c_double, C.c_double, _P]),
 }

@@ -299,6 +299,20 @@ class Engine:
         _lib.check(self.lib.capgen_debug_collectives(self.h, int(op), buf, cap))
         return buf.value.decode()
 
+    def stamps(self, op: int):
+        """Diagnostic un-profiled timeline (capgen_debug_stamps): op 1 on, 0 off, 3 arm; op 2 returns
+        [(name, start_us, end_us)] of the last step's stamped launches (unlaunched slots: 0, 0)."""
+        cap = 8192
+        out = np.zeros(2 * cap, np.float64)
+        names = C.create_string_buffer(1 << 20)
+        n = self.lib.capgen_debug_stamps(self.h, int(op), out.ctypes.data_as(C.c_void_p), 2 * cap, names, 1 << 20)
+        if n < 0:
+            _lib.check(1)
+        if op != 2:
+            return None
+        lines = names.value.decode().split("\n")
+        return [(lines[i], out[2 * i], out[2 * i + 1]) for i in range(n)]
+
     def dp_debug_shard(self, rank: int, world: int):
         """Test hook: update as rank `rank` of `world` would under the sharded update, no collectives."""
         _lib.check(self.lib.capgen_dp_debug_shard(self.h, int(rank), int(world)))

@@ -23,6 +23,7 @@ struct AttnGeom {
   int causal = 0, q_pos0 = 0;         // mask keys j > q_pos0 + i
   float temperature = 1.f;            // sqrt(dk), q is divided by it (modules.py:18,56)
   Drop drop{};                        // dropout on the probabilities (modules.py:24)
+  uint64_t* stamp = nullptr;          // diagnostic timestamps (StampScope)
 };
 
 // probs (optional): [B,H,Lq,Lk] f32, pre-dropout softmax, saved for backward / attention_list.

@@ -149,6 +149,7 @@ __device__ __forceinline__ void store4(bf16* p, f32x4 v, float mul) {
 __global__ void __launch_bounds__(256) attn_fwd_mfma_kernel(AttnGeom g, bf16* __restrict__ o,
                                                             float* __restrict__ probs) {
   __shared__ __attribute__((aligned(16))) char sm[3 * IMG + 64];
+  StampScope stamp_scope(g.stamp);
   if (g.prio) __builtin_amdgcn_s_setprio(3);
   char* Qimg = sm;
   char* Kimg = sm + IMG;
@@ -210,6 +211,7 @@ __global__ void __launch_bounds__(256) attn_bwd_mfma_kernel(AttnGeom g, const bf
                                                             bf16* __restrict__ dq, bf16* __restrict__ dkp,
                                                             bf16* __restrict__ dvp) {
   __shared__ __attribute__((aligned(16))) char sm[6 * IMG + 64];
+  StampScope stamp_scope(g.stamp);
   if (g.prio) __builtin_amdgcn_s_setprio(3);
   char* Kimg = sm;             // [key][d]
   char* dOimg = sm + IMG;      // [q][d]

@@ -31,6 +31,22 @@ inline void require(bool ok, const std::string& what) {
 // 128 LayerNorm-backward gamma/beta/bias sums.
 int skip_mask();
 
+// ---- diagnostic in-kernel timestamps (capgen_debug_stamps) --------------------------------
+// A launch given a stamp slot (16 x u64) records the 100 MHz real-time counter: [0] when block 0
+// starts, [1 + (block % 8)] the latest block end of that residue class (atomic max).  nullptr:
+// nothing is recorded (one uniform branch per block).
+__device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
+struct StampScope {
+  uint64_t* p;
+  __device__ __forceinline__ explicit StampScope(uint64_t* q) : p(q) {
+    if (p && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) p[0] = rt_now();
+  }
+  __device__ __forceinline__ ~StampScope() {
+    if (p && threadIdx.x == 0)
+      atomicMax(reinterpret_cast<unsigned long long*>(p) + 1 + (blockIdx.x & 7), (unsigned long long)rt_now());
+  }
+};
+
 // ---- scalar conversions -------------------------------------------------------------
 __device__ __forceinline__ float to_f(float x) { return x; }
 __device__ __forceinline__ float to_f(bf16 x) { return (float)x; }

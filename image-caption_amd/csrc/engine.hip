@@ -349,13 +349,35 @@ struct capgen_engine {
     return !(e && e[0] == '0');
   }();
 
+  // diagnostic in-kernel timestamps (capgen_debug_stamps): every GEMM / LayerNorm / attention
+  // launch of a step gets a slot of the ring (forward slots first: a captured forward graph keeps
+  // its slots, the backward re-numbers from where the forward ended); names for the report
+  bool stamp_on = false;
+  uint64_t* stamp_ring = nullptr;
+  static constexpr int kStampSlots = 4096;
+  int stamp_next = 0, stamp_fwd_end = 0, stamp_max = 0;
+  std::vector<std::string> stamp_names;
+  uint64_t* stamp(hipStream_t s, const std::string& what) {
+    if (!stamp_on || !stamp_ring || stamp_next >= kStampSlots) return nullptr;
+    const int i = stamp_next++;
+    stamp_max = std::max(stamp_max, stamp_next);
+    if ((int)stamp_names.size() <= i) stamp_names.resize(i + 1);
+    stamp_names[i] = std::string(s == ec && ec != es2 ? "bucket " : s == es2 && es2 != (crit ? crit : es) ? "side " : "crit ") + what;
+    return stamp_ring + (size_t)i * 16;
+  }
+  static std::string dims(int M, int N, int K) {
+    return std::to_string(M) + "x" + std::to_string(N) + "x" + std::to_string(K);
+  }
+
   // the row / attention kernels with the launch's issue priority (prio above)
-  void lnf(LnFwd l, hipStream_t s) const {
+  void lnf(LnFwd l, hipStream_t s) {
     l.prio = prio(s);
+    if (stamp_on) l.stamp = stamp(s, "ln_fwd " + std::to_string(l.M));
     layernorm_fwd(l, act, s);
   }
-  void lnb(LnBwd l, hipStream_t s) const {
+  void lnb(LnBwd l, hipStream_t s) {
     l.prio = prio(s);
+    if (stamp_on) l.stamp = stamp(s, "ln_bwd " + std::to_string(l.M));
     layernorm_bwd(l, act, s);
   }
   // CAPGEN_LN_SUMS_SIDE=1 (experiment, off): a transformer block's LayerNorm backward on the
@@ -382,13 +404,15 @@ struct capgen_engine {
     side.mask = RowMask{};
     lns_pending.push_back(side);
   }
-  void attf(AttnGeom g, void* o, float* probs, DType t, hipStream_t s) const {
+  void attf(AttnGeom g, void* o, float* probs, DType t, hipStream_t s) {
     g.prio = prio(s);
+    if (stamp_on) g.stamp = stamp(s, "attn_fwd " + std::to_string(g.Lq) + "x" + std::to_string(g.Lk));
     attention_fwd(g, o, probs, t, s);
   }
   void attb(AttnGeom g, const float* probs, const void* dout, void* dq, void* dk, void* dv, DType t,
-            hipStream_t s) const {
+            hipStream_t s) {
     g.prio = prio(s);
+    if (stamp_on) g.stamp = stamp(s, "attn_bwd " + std::to_string(g.Lq) + "x" + std::to_string(g.Lk));
     attention_bwd(g, probs, dout, dq, dk, dv, t, s);
   }
 
@@ -400,6 +424,7 @@ struct capgen_engine {
     ga.bias = bias;
     ga.relu = relu;
     ga.prio = prio(s);
+    if (stamp_on) ga.stamp = stamp(s, "gemm fwd " + dims(M, N, K));
     gemm(ga, act, tout, false, false, s);
   }
   // C = X . W^T into ln.a, then y = LayerNorm(drop(C + bias) + res (+ pe)) (modules.py:86-90).
@@ -433,6 +458,7 @@ struct capgen_engine {
     ga.ldaux = ldx;
     ga.alpha_ptr = alpha_ptr;
     ga.prio = prio(s);
+    if (stamp_on) ga.stamp = stamp(s, "gemm dX " + dims(M, K, N));
     gemm(ga, act, act, false, true, s);
   }
   // dW[N,K] = alpha * dY[M,N]^T . X[M,K]   (f32, overwrites)
@@ -442,6 +468,7 @@ struct capgen_engine {
     ga.M = N, ga.N = K, ga.K = M, ga.A = dY, ga.lda = ldy, ga.B = X, ga.ldb = ldx, ga.C = G(goff), ga.ldc = ldg;
     ga.alpha_ptr = alpha_ptr;
     ga.prio = prio(s);
+    if (stamp_on) ga.stamp = stamp(s, "gemm dW " + dims(N, K, M));
     gemm(ga, act, DType::F32, true, true, s);
   }
 
@@ -777,6 +804,7 @@ struct capgen_engine {
     const int Lq = T - 1, Me = B * N, Md = B * Lq, d = L.d, dd = L.dd;
     const int He = L.He, Hd = L.Hd, dke = d / He, dkd = dd / Hd;
     fB = B, fN = N, fT = T, fwd_drop = drop_on;
+    stamp_next = 0;
     const float p = cfg.dropout, pa = cfg.attention_dropout;
 
     // (+ the dropout seed advance when dropout is on: the pack kernel does not read the seed, every
@@ -909,6 +937,7 @@ struct capgen_engine {
       ga.M = Md, ga.N = L.V, ga.K = dd, ga.A = dec_out(), ga.lda = dd, ga.B = W(L.Wc), ga.ldb = dd;
       ga.C = a.dlogits, ga.ldc = L.V, ga.bias = P(L.bc), ga.prio = prio(s);
       ga.ce_stats = a.ce_stats, ga.ce_ld = (L.V + 15) / 16, ga.ce_tgt = a.tgt, ga.ce_tlogit = a.ce_tl;
+      if (stamp_on) ga.stamp = stamp(s, "gemm classifier+CE " + dims(Md, L.V, dd));
       gemm(ga, act, act, false, false, s);
       ce_finish(a.ce_stats, (L.V + 15) / 16, a.ce_tl, a.tgt, Md, L.V, cfg.pad_idx, a.loss_row,
                 reinterpret_cast<bf16*>(a.dlogits), s);
@@ -928,6 +957,7 @@ struct capgen_engine {
     } else {
       loss_finalize(a.loss_row, Md, a.count, cfg.focal_loss, lo, a.grad_scale, s);
     }
+    stamp_fwd_end = stamp_next;
   }
 
   // ------------------------------------------------------------------------------------
@@ -1002,8 +1032,10 @@ struct capgen_engine {
     if (act == DType::BF16 && group_dw) {
       std::vector<GemmArgs> probs;
       for (size_t i = 0; i < n; ++i) probs.push_back(dw_args(jobs[i]));
-      for (size_t i = 0; i < n; i += kMaxGroup)
+      for (size_t i = 0; i < n; i += kMaxGroup) {
+        if (stamp_on) probs[i].stamp = stamp(st, "gemm dW group of " + std::to_string(std::min<size_t>(kMaxGroup, n - i)));
         gemm_grouped(probs.data() + i, (int)std::min<size_t>(kMaxGroup, n - i), DType::F32, true, true, st);
+      }
     } else {
       for (size_t i = 0; i < n; ++i) {
         const DwJob& j = jobs[i];
@@ -1272,6 +1304,7 @@ struct capgen_engine {
     bstep = step_params;
     require(fB > 0, "backward: call forward first");
     grads_sharded = false;
+    stamp_next = stamp_fwd_end;
     const int B = fB, N = fN, Lq = fT - 1, Me = B * N, Md = B * Lq, d = L.d, dd = L.dd;
     const int He = L.He, Hd = L.Hd, dke = d / He, dkd = dd / Hd;
     const bool on = fwd_drop;
@@ -1421,6 +1454,7 @@ struct capgen_engine {
       hz::wait(s, ev_part);
       GemmArgs ga = dx_args(a.gKV, kvld, L.Wkv_all, d, gO, d, Me, 2 * dd, d, 0);
       ga.cin = a.gEnc32, ga.ldcin = d, ga.prio = prio(s);
+      if (stamp_on) ga.stamp = stamp(s, "gemm dX " + dims(Me, d, 2 * dd));
       gemm(ga, act, act, false, true, s);
     } else {
       linear_dx(a.gKV, kvld, L.Wkv_all, d, gO, d, Me, L.Ld * 2 * dd, d, 0, nullptr, nullptr, s);
@@ -1914,7 +1948,7 @@ struct capgen_engine {
     drop_graph();
     if (comm) ncclCommDestroy(comm);
     for (void* p : {(void*)params, (void*)grads, (void*)am, (void*)av, (void*)shadow, (void*)pe, (void*)step,
-                    (void*)adam_scal, (void*)seed, (void*)scalars, (void*)gstripe, ws, gws})
+                    (void*)adam_scal, (void*)seed, (void*)scalars, (void*)gstripe, ws, gws, (void*)stamp_ring})
       if (p) (void)hipFree(p);
     if (count_host) (void)hipHostFree(count_host);
     if (ev_in) (void)hipEventDestroy(ev_in);
@@ -2415,6 +2449,48 @@ int capgen_debug_collectives(capgen_t* h, int op, char* out, int cap) {
       out[k] = 0;
     }
   });
+}
+
+int capgen_debug_stamps(capgen_t* h, int op, double* out, int cap, char* names, int names_cap) {
+  int count = 0;
+  const int rc = guarded([&] {
+    require(h != nullptr, "null engine handle");
+    require(op >= 0 && op <= 3, "debug_stamps: op 0 (off), 1 (on), 2 (read), 3 (arm)");
+    set_device(h);
+    if (op == 0 || op == 1) {
+      hz::host_sync(nullptr);
+      h->stamp_on = op == 1;
+      if (h->stamp_on && !h->stamp_ring)
+        CAPGEN_HIP(hipMalloc(&h->stamp_ring, (size_t)capgen_engine::kStampSlots * 16 * sizeof(uint64_t)));
+      h->drop_graph();  // a captured forward holds its launches' stamp pointers
+    }
+    if (op == 3 || op == 1) {
+      hz::host_sync(nullptr);
+      if (h->stamp_ring) CAPGEN_HIP(hipMemset(h->stamp_ring, 0, (size_t)capgen_engine::kStampSlots * 16 * sizeof(uint64_t)));
+      CAPGEN_HIP(hipDeviceSynchronize());
+    }
+    if (op == 2) {
+      require(h->stamp_ring != nullptr, "debug_stamps: not enabled");
+      hz::host_sync(nullptr);
+      std::vector<uint64_t> ring((size_t)h->stamp_max * 16);
+      CAPGEN_HIP(hipMemcpy(ring.data(), h->stamp_ring, ring.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+      std::string all;
+      for (int i = 0; i < h->stamp_max && 2 * i + 1 < cap; ++i) {
+        uint64_t e = 0;
+        for (int k = 1; k <= 8; ++k) e = std::max(e, ring[(size_t)i * 16 + k]);
+        out[2 * i] = (double)ring[(size_t)i * 16] * 0.01;  // 100 MHz ticks -> us
+        out[2 * i + 1] = (double)e * 0.01;
+        all += (i < (int)h->stamp_names.size() ? h->stamp_names[i] : std::string("?")) + "\n";
+        ++count;
+      }
+      if (names && names_cap > 0) {
+        const size_t k = std::min<size_t>(all.size(), (size_t)names_cap - 1);
+        std::memcpy(names, all.data(), k);
+        names[k] = 0;
+      }
+    }
+  });
+  return rc ? -1 : count;
 }
 
 int capgen_debug_side_delay(double us) {

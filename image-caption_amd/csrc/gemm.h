@@ -40,6 +40,7 @@ struct GemmArgs {
   int64_t ce_ld = 0;
   const int32_t* ce_tgt = nullptr;
   float* ce_tlogit = nullptr;
+  uint64_t* stamp = nullptr;  // diagnostic timestamps (capgen_common.h StampScope); grouped: p[0]'s
 };
 
 // Independent GEMMs of one layout launched as ONE grid (tiles problem after problem).

@@ -505,6 +505,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmArgs g, int
                                                                 const void* zero, int splitk, float* ws,
                                                                 int* tile_cnt, int group_m, int proto) {
   __shared__ __attribute__((aligned(1024))) char smem[TileCfg<TA, TB, BM, BN, WM, WN, STAGES>::SMEM];
+  StampScope stamp_scope(g.stamp);
   // critical-path launch (GemmArgs::prio): beside the side streams' weight-gradient / Adam waves
   // on the same CUs, the SIMD arbiter issues this kernel's instructions first
   if (g.prio) __builtin_amdgcn_s_setprio(3);
@@ -530,6 +531,7 @@ template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int STA
 __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_grouped_kernel(GemmGroup gg, int nblk, int G,
                                                                         const void* zero) {
   __shared__ __attribute__((aligned(1024))) char smem[TileCfg<TA, TB, BM, BN, WM, WN, STAGES>::SMEM];
+  StampScope stamp_scope(gg.p[0].stamp);
   for (int b = blockIdx.x; b < nblk; b += G) {
     if (b != (int)blockIdx.x) __syncthreads();  // the previous tile's LDS reads are done
     const int slot = xcd_slot(b, nblk);
@@ -810,6 +812,7 @@ static Choice tune(const GemmArgs& g, hipStream_t s) {
   t.C = scratch;
   t.beta = 0;
   t.colsum = nullptr;
+  t.stamp = nullptr;
   hipEvent_t e0, e1;
   CAPGEN_HIP(hipEventCreate(&e0));
   CAPGEN_HIP(hipEventCreate(&e1));
@@ -1006,7 +1009,7 @@ static void launch_group(const GemmArgs* ps, int n, hipStream_t s) {
         std::vector<void*> scratch(n);
         for (int i = 0; i < n; ++i) {
           CAPGEN_HIP(hipMalloc(&scratch[i], (size_t)t[i].M * t[i].ldc * sizeof(TO)));
-          t[i].C = scratch[i], t[i].beta = 0, t[i].colsum = nullptr;
+          t[i].C = scratch[i], t[i].beta = 0, t[i].colsum = nullptr, t[i].stamp = nullptr;
         }
         hipEvent_t e0, e1;
         CAPGEN_HIP(hipEventCreate(&e0));

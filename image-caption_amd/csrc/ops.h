@@ -22,6 +22,7 @@ struct LnFwd {
   void* v_save = nullptr;  // LN input (post residual add), saved for backward
   float* mean = nullptr;
   float* rstd = nullptr;
+  uint64_t* stamp = nullptr;  // diagnostic timestamps (StampScope)
 };
 void layernorm_fwd(const LnFwd& a, DType t, hipStream_t s);
 
@@ -44,6 +45,7 @@ struct LnBwd {
   int stripes = 1;
   int64_t stripe_stride = 0;
   void* y_save = nullptr;  // optional: the masked output gradient dy * rowmask (T), for layernorm_param_sums
+  uint64_t* stamp = nullptr;  // diagnostic timestamps (StampScope)
 };
 void layernorm_bwd(const LnBwd& a, DType t, hipStream_t s);
 // The LayerNorm parameter sums alone -- dgamma += sum y * xhat, dbeta += sum y, dbias += sum d_a --

@@ -34,6 +34,7 @@ __device__ __forceinline__ void load_f32(const float* p, float (&out)[DPL]) {
 }
 template <typename T, int DPL>
 __global__ void __launch_bounds__(LN_THREADS) ln_fwd_kernel(LnFwd a) {
+  StampScope stamp_scope(a.stamp);
   if (a.prio) __builtin_amdgcn_s_setprio(3);
   const int lane = threadIdx.x & 63;
   const int m = blockIdx.x * (LN_THREADS / 64) + (threadIdx.x >> 6);
@@ -93,6 +94,7 @@ __global__ void __launch_bounds__(LN_THREADS) ln_fwd_kernel(LnFwd a) {
 template <typename T, int DPL, int R, int NT = LN_THREADS>  // R rows in flight per wave: every load of them is issued first
 __global__ void __launch_bounds__(NT) ln_bwd_kernel(LnBwd a) {
   __shared__ float red[3][NT / 64][64 * DPL];
+  StampScope stamp_scope(a.stamp);
   if (a.prio) __builtin_amdgcn_s_setprio(3);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int d = a.d, c0 = lane * DPL;

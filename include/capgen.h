@@ -228,6 +228,12 @@ int capgen_debug_side_delay(double us);
  * collective: name, bytes, stream role).  Every rank must issue the identical sequence whatever its
  * batch, or the ranks deadlock (test hook for the data-parallel step). */
 int capgen_debug_collectives(capgen_t* h, int op, char* out, int cap);
+/* Un-profiled per-kernel timeline: op 1 = give every GEMM / LayerNorm / attention launch of the
+ * following steps a timestamp slot (drops the captured forward so it re-captures with them), 3 = arm
+ * (zero the slots; device synchronised), 2 = read: out[2i], out[2i+1] = start / end (us, 100 MHz
+ * real-time counter) of slot i of the last step, names = one line per slot ("crit|side|bucket
+ * kernel shape"); returns the slot count (-1: error), 0 = off. */
+int capgen_debug_stamps(capgen_t* h, int op, double* out, int cap, char* names, int names_cap);
 
 /* Data parallel (one process per GPU, RCCL over xGMI).  Rank 0 creates the 128-byte
  * unique id; the host broadcasts it (torch.distributed store) and every rank calls
