@@ -2390,7 +2390,7 @@ int capgen_debug_splitk_diag(int* out4, int reset) {
 
 int capgen_debug_splitk_protocol(int proto) {
   return guarded([&] {
-    require(proto >= 0 && proto < 1024, "debug_splitk_protocol: bits 0..9 only");
+    require(proto >= 0 && proto < 4096, "debug_splitk_protocol: bits 0..11 only (10, 11: ablation build)");
     gemm_set_splitk_protocol(proto);
   });
 }

@@ -214,6 +214,17 @@ template <typename TO, int FM, int FN, int TM, int TN>
 __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&acc)[FM][FN], int m0, int n0, int wm,
                                               int wn, int lane, float alpha);
 
+// Diagnostic ablation build (make ablate -> libcapgen_ablate.so, tools/gemm_ablate.py): protocol bit
+// 1024 skips the MFMAs, bit 2048 skips the operand DMA and its waits -- what a shape costs without
+// its arithmetic, without its operand ingest, or with neither (the launch + epilogue intercept).
+#ifdef CAPGEN_GEMM_ABLATE
+#define ABL_NO_MFMA (proto & 1024)
+#define ABL_NO_DMA (proto & 2048)
+#else
+#define ABL_NO_MFMA 0
+#define ABL_NO_DMA 0
+#endif
+
 // diagnostic counters of the split-K hand-off (protocol bit 64): [0] tickets found >= splitk at
 // arrival (a ticket not re-armed before this launch), [1] tiles combined
 __device__ int g_sk_diag[4];
@@ -255,6 +266,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int mt, int nt, int
   oa.setup(A, g.lda, m0, g.M, g.K, kt0, wave, lane);
   ob.setup(B, g.ldb, n0, g.N, g.K, kt0, wave, lane);
   auto issue = [&](int t, char* st) {
+    if (ABL_NO_DMA) return;
     const int kb = (kt0 + t) * BK;
     const bool tail = kb + BK > g.K;
     oa.issue(t, st, tail, kb, g.K, wave);
@@ -273,7 +285,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int mt, int nt, int
       const int kt = kb + s;
       if (kt < nk) {
         // tile kt landed for this wave (up to STAGES-2 younger tiles may still fly) ...
-        wait_younger<LPT, STAGES - 2>(nk - 1 - kt);
+        if (!ABL_NO_DMA) wait_younger<LPT, STAGES - 2>(nk - 1 - kt);
         __builtin_amdgcn_s_barrier();  // ... for every wave; stage (s-1) % STAGES is free again
         if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, smem + ((s + STAGES - 1) % STAGES) * SB);
         const char* st = smem + s * SB;
@@ -284,6 +296,13 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int mt, int nt, int
           for (int i = 0; i < FM; ++i) af[i] = OA::frag(st, wm * TM + i * 16, ks, lane);
 #pragma unroll
           for (int j = 0; j < FN; ++j) bfr[j] = OB::frag(st + OA::BYTES, wn * TN + j * 16, ks, lane);
+          if (ABL_NO_MFMA) {  // (ablation: keep the fragment reads live)
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+              for (int j = 0; j < FN; ++j) acc[i][j][0] += (float)af[i][0] + (float)bfr[j][0];
+            continue;
+          }
 #pragma unroll
           for (int i = 0; i < FM; ++i)
 #pragma unroll
