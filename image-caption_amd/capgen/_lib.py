@@ -73,6 +73,7 @@ _SIGS = {
     "capgen_debug_gemm_variant": (C.c_int, [C.c_int]),
     "capgen_debug_splitk_protocol": (C.c_int, [C.c_int]),
     "capgen_debug_splitk_diag": (C.c_int, [_P, C.c_int]),
+    "capgen_debug_gemm_timing_buf": (C.c_int, [_P]),
     "capgen_debug_copy_buffer": (C.c_int, [_P, C.c_int, _P, C.c_int64]),
     "capgen_train_step_indexed": (C.c_int, [_P, _P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int, _P,
                                             _P]),

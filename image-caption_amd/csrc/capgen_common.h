@@ -1,6 +1,7 @@
 // capgen — shared device/host helpers for the gfx950 (MI355X, CDNA4) kernels.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <stdint.h>
 #include <string>
 
@@ -49,7 +50,38 @@ struct StampScope {
   }
 };
 
+// ---- write-through output stores ----------------------------------------------------------
+// A plain store leaves its line dirty in the writing XCD's L2 and the end of the launch writes every
+// such line back before the next dependent launch may start (MI355X_MICROARCH.md price list,
+// 'boundary': + B / 6 TB/s for B dirty bytes).  An sc1 buffer store writes through at once
+// (16-B sc1 store ~ plain store, same table), overlapped with the rest of the launch.  The base
+// must be wave-uniform (a kernel argument); offsets are bytes (< 2 GB).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7FFFFFFF, 0x00020000);
+}
+typedef __attribute__((ext_vector_type(2))) unsigned int wt_u32x2;
+typedef __attribute__((ext_vector_type(4))) unsigned int wt_u32x4;
+__device__ __forceinline__ void wt_store8(__amdgpu_buffer_rsrc_t r, uint32_t off, wt_u32x2 v) {
+  __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, 16 /* sc1 */);
+}
+__device__ __forceinline__ void wt_store16(__amdgpu_buffer_rsrc_t r, uint32_t off, wt_u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16 /* sc1 */);
+}
+// N consecutive elements of T at byte offset `off` from the rsrc base (16-B pieces), write-through
+template <typename T, int N>
+__device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, uint32_t off, const float (&in)[N]);
+// write-through default: off (CAPGEN_WT=1 enables; measured slower in the step, 4-round A/B 3.16-3.22
+// vs 3.04-3.17 ms: the end-of-launch write-back is not what the ~3 us kernel boundary is made of)
+inline int wt_default() {
+  static const int on = [] {
+    const char* e = std::getenv("CAPGEN_WT");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 // ---- scalar conversions -------------------------------------------------------------
+// (store_wt after the conversions below)
 __device__ __forceinline__ float to_f(float x) { return x; }
 __device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
 template <typename T> __device__ __forceinline__ T from_f(float x);
@@ -93,6 +125,21 @@ __device__ __forceinline__ void store_f(T* p, const float (&in)[N]) {
   } else {
 #pragma unroll
     for (int i = 0; i < N; ++i) p[i] = from_f<T>(in[i]);
+  }
+}
+
+template <typename T, int N>
+__device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, uint32_t off, const float (&in)[N]) {
+  constexpr int PER = 16 / sizeof(T);  // elements per 16-B piece
+  static_assert(N % PER == 0, "store_wt: whole 16-B pieces");
+#pragma unroll
+  for (int p = 0; p < N / PER; ++p) {
+    typedef typename Vec16<T>::type V;
+    V v;
+    T* e = reinterpret_cast<T*>(&v);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) e[i] = from_f<T>(in[p * PER + i]);
+    wt_store16(r, off + p * 16, __builtin_bit_cast(wt_u32x4, v));
   }
 }
 

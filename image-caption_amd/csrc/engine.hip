@@ -2384,13 +2384,17 @@ int capgen_debug_copy_buffer(capgen_t* h, int which, void* host_dst, int64_t byt
   });
 }
 
+int capgen_debug_gemm_timing_buf(void* dev_buf) {
+  return guarded([&] { gemm_set_timing_buf(reinterpret_cast<uint64_t*>(dev_buf)); });
+}
+
 int capgen_debug_splitk_diag(int* out4, int reset) {
   return guarded([&] { gemm_splitk_diag(out4, reset != 0); });
 }
 
 int capgen_debug_splitk_protocol(int proto) {
   return guarded([&] {
-    require(proto >= 0 && proto < 4096, "debug_splitk_protocol: bits 0..11 only (10, 11: ablation build)");
+    require(proto >= 0 && proto < 8192, "debug_splitk_protocol: bits 0..12 only (10-12: ablation build)");
     gemm_set_splitk_protocol(proto);
   });
 }

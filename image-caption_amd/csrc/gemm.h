@@ -41,6 +41,7 @@ struct GemmArgs {
   const int32_t* ce_tgt = nullptr;
   float* ce_tlogit = nullptr;
   uint64_t* stamp = nullptr;  // diagnostic timestamps (capgen_common.h StampScope); grouped: p[0]'s
+  int wt = -1;                // write-through (sc1) C stores (bf16 path): 1/0, -1 = wt_default()
 };
 
 // Independent GEMMs of one layout launched as ONE grid (tiles problem after problem).
@@ -61,6 +62,8 @@ void gemm_init();
 void gemm_set_variant(int v);
 // diagnostic: split-K hand-off protocol bits (0 = the full recipe; gemm_bf16.hip g_splitk_proto)
 void gemm_set_splitk_protocol(int p);
+// diagnostic (ablation build, protocol bit 4096): device buffer of >= 88 u64 for the phase timestamps
+void gemm_set_timing_buf(uint64_t* p);
 // diagnostic: read (and optionally zero) the split-K hand-off counters (protocol bit 64)
 void gemm_splitk_diag(int* out4, bool reset);
 // n <= kMaxGroup independent bf16-operand GEMMs of one layout / output type in one launch

@@ -200,29 +200,51 @@ __device__ __forceinline__ void store4(TO* p, const float (&v)[4]) {
 
 }  // namespace
 
-// Tile geometry of one variant (shared by the plain and the grouped launch).
-template <bool TA, bool TB, int BM, int BN, int WM, int WN, int STAGES>
+// Tile geometry of one variant (shared by the plain and the grouped launch).  KG k-groups: the
+// workgroup holds KG groups of WM x WN waves; group g runs the k-loop over the g-th contiguous
+// chunk of the tile's k-tiles with its own LDS ring (the per-workgroup k-chain is latency-bound --
+// tools/gemm_phase_timing.py: ~1000 cycles per 64-deep step of a 64x64 tile, time independent of M
+// -- so KG chains of nk/KG steps run side by side on the same CU), then the groups sum their
+// partial tiles through LDS in group order (bit-identical to grid split-K with KG slices) and each
+// group stores 1/KG of the tile's fragments.
+template <bool TA, bool TB, int BM, int BN, int WM, int WN, int STAGES, int KG = 1>
 struct TileCfg {
-  static constexpr int NW = WM * WN;
+  static constexpr int NW = WM * WN;  // waves per k-group
+  static constexpr int NWT = NW * KG;  // waves per workgroup
   typedef Op<TA, BM, NW> OA;
   typedef Op<TB, BN, NW> OB;
   static constexpr int SB = OA::BYTES + OB::BYTES;  // LDS bytes per stage
-  static constexpr int SMEM = STAGES * SB;
+  static constexpr int XCH = KG > 1 ? (BM / WM / 16) * (BN / WN / 16) * KG * NW * 64 * 16 : 0;  // k-group exchange
+  static constexpr int SMEM = KG * STAGES * SB > XCH ? KG * STAGES * SB : XCH;
 };
 
 template <typename TO, int FM, int FN, int TM, int TN>
 __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&acc)[FM][FN], int m0, int n0, int wm,
-                                              int wn, int lane, float alpha);
+                                              int wn, int lane, float alpha, int kgrp = 0, int kgs = 1);
 
 // Diagnostic ablation build (make ablate -> libcapgen_ablate.so, tools/gemm_ablate.py): protocol bit
 // 1024 skips the MFMAs, bit 2048 skips the operand DMA and its waits -- what a shape costs without
 // its arithmetic, without its operand ingest, or with neither (the launch + epilogue intercept).
+// Bit 4096 (same build): wave 0 of block 0 records s_memtime / s_memrealtime at the kernel start, after
+// the prologue DMA issue, at four points of each of the first 8 k-steps (after the DMA wait, after
+// the barrier, after the next stage's DMA issue, after the MFMAs) and after the epilogue, into
+// g.stamp[16 ..] (gemm_set_timing_buf): cycles per phase and the in-kernel clock.
 #ifdef CAPGEN_GEMM_ABLATE
 #define ABL_NO_MFMA (proto & 1024)
 #define ABL_NO_DMA (proto & 2048)
+#define ABL_T(slot)                                                                                   \
+  do {                                                                                                \
+    if ((proto & 4096) && g.stamp && blockIdx.x == 0 && threadIdx.x == 0) {                           \
+      g.stamp[16 + 2 * (slot)] = __builtin_amdgcn_s_memtime();                                        \
+      g.stamp[17 + 2 * (slot)] = __builtin_amdgcn_s_memrealtime();                                    \
+    }                                                                                                 \
+  } while (0)
 #else
 #define ABL_NO_MFMA 0
 #define ABL_NO_DMA 0
+#define ABL_T(slot) \
+  do {              \
+  } while (0)
 #endif
 
 // diagnostic counters of the split-K hand-off (protocol bit 64): [0] tickets found >= splitk at
@@ -231,10 +253,10 @@ __device__ int g_sk_diag[4];
 
 // One BMxBN output tile (split-K slice `split` of `splitk`) of C = op(A).op(B): the LDS-DMA
 // ring, the MFMA main loop and the epilogue (in-launch split-K combine included).
-template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int STAGES>
+template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int STAGES, int KG = 1>
 __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int mt, int nt, int tile, int split, int splitk,
                                           const void* zero, float* ws, int* tile_cnt, char* smem, int proto = 0) {
-  typedef TileCfg<TA, TB, BM, BN, WM, WN, STAGES> Cfg;
+  typedef TileCfg<TA, TB, BM, BN, WM, WN, STAGES, KG> Cfg;
   constexpr int NW = Cfg::NW;
   typedef typename Cfg::OA OA;
   typedef typename Cfg::OB OB;
@@ -245,10 +267,13 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int mt, int nt, int
   static_assert(STAGES >= 2, "need >= 2 stages");
   const int m0 = mt * BM, n0 = nt * BN;
 
+  ABL_T(0);
   const bf16* __restrict__ A = reinterpret_cast<const bf16*>(g.A);
   const bf16* __restrict__ B = reinterpret_cast<const bf16*>(g.B);
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wave_all = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int kgrp = KG > 1 ? wave_all / NW : 0;  // k-group of this wave
+  const int wave = KG > 1 ? wave_all % NW : wave_all;
   const int wm = wave / WN, wn = wave % WN;
 
   f32x4 acc[FM][FN];
@@ -259,8 +284,11 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int mt, int nt, int
 
   const int nk_all = (g.K + BK - 1) / BK;
   const int per = (nk_all + splitk - 1) / splitk;
-  const int kt0 = split * per;
-  const int nk = max(0, min(nk_all - kt0, per));  // K tiles of this slice
+  const int nks = max(0, min(nk_all - split * per, per));  // K tiles of this slice
+  const int per_g = (nks + KG - 1) / KG;                    // ... of each k-group (the loop's trip count)
+  const int kt0 = split * per + kgrp * per_g;               // this group's first k-tile
+  const int nk = max(0, min(nks - kgrp * per_g, per_g));    // this group's k-tiles (<= per_g)
+  if (KG > 1) smem += kgrp * (STAGES * SB);                 // the group's LDS ring
   OA oa;
   OB ob;
   oa.setup(A, g.lda, m0, g.M, g.K, kt0, wave, lane);
@@ -275,22 +303,29 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int mt, int nt, int
 #pragma unroll
   for (int p = 0; p < STAGES - 1; ++p)
     if (p < nk) issue(p, smem + p * SB);
+  ABL_T(1);
 
   // k-loop unrolled by STAGES: tile kb + s lives in stage s, so every LDS offset is a constant
   // (ds_read immediate offsets, a scalar M0 per DMA piece: no address VALU in the loop)
   static_assert((STAGES - 2) * LPT <= 63, "vmcnt range");
-  for (int kb = 0; kb < nk; kb += STAGES) {
+  // (every k-group runs per_g trips -- the barriers stay uniform -- and works on its own nk)
+  for (int kb = 0; kb < per_g; kb += STAGES) {
 #pragma unroll
     for (int s = 0; s < STAGES; ++s) {
       const int kt = kb + s;
-      if (kt < nk) {
+      if (kt < per_g) {
+        const bool work = KG == 1 || kt < nk;
         // tile kt landed for this wave (up to STAGES-2 younger tiles may still fly) ...
-        if (!ABL_NO_DMA) wait_younger<LPT, STAGES - 2>(nk - 1 - kt);
+        if (!ABL_NO_DMA && work) wait_younger<LPT, STAGES - 2>(nk - 1 - kt);
+        if (kt < 8) ABL_T(2 + 4 * kt);
         __builtin_amdgcn_s_barrier();  // ... for every wave; stage (s-1) % STAGES is free again
+        if (kt < 8) ABL_T(3 + 4 * kt);
         if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, smem + ((s + STAGES - 1) % STAGES) * SB);
+        if (kt < 8) ABL_T(4 + 4 * kt);
         const char* st = smem + s * SB;
 #pragma unroll
         for (int ks = 0; ks < BK / 32; ++ks) {
+          if (!work) break;
           bf16x8 af[FM], bfr[FN];
 #pragma unroll
           for (int i = 0; i < FM; ++i) af[i] = OA::frag(st, wm * TM + i * 16, ks, lane);
@@ -309,12 +344,42 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int mt, int nt, int
             for (int j = 0; j < FN; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
         }
+        if (kt < 8) ABL_T(5 + 4 * kt);
       }
     }
   }
+  ABL_T(34);
 
   // ---- epilogue: lane holds C[m = mb + (lane&15)][n = nb + 4*(lane>>4) + 0..3] ----
   const float alpha = g.alpha_ptr ? g.alpha * *g.alpha_ptr : g.alpha;
+  if constexpr (KG > 1) {
+    // k-group exchange: fragment f = i * FN + j belongs to group f % KG; every group parks the
+    // fragments it does not own in LDS (the rings are idle: every DMA was waited for, every
+    // fragment read consumed), then each owner sums the KG partials in group order
+    if (KG > 1) smem -= kgrp * (STAGES * SB);
+    f32x4* ex = reinterpret_cast<f32x4*>(smem);
+    constexpr int NF = FM * FN;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        if ((i * FN + j) % KG != kgrp) ex[(((i * FN + j) * KG + kgrp) * NW + wave) * 64 + lane] = acc[i][j];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        if ((i * FN + j) % KG != kgrp) continue;
+        f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int h = 0; h < KG; ++h) sum += h == kgrp ? acc[i][j] : ex[(((i * FN + j) * KG + h) * NW + wave) * 64 + lane];
+        acc[i][j] = sum;
+      }
+    tile_epilogue<TO, FM, FN, TM, TN>(g, acc, m0, n0, wm, wn, lane, alpha, kgrp, KG);
+    ABL_T(35);
+    return;
+  }
   if (splitk > 1) {
     // Split-K combine inside the launch (the guide's counter hand-off, cdna_hip_programming.md
     // §5 'Projection GEMM' item 2 / §6 Guideline 16): every slice stores its raw partial tile
@@ -399,16 +464,18 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int mt, int nt, int
       }
   }
   tile_epilogue<TO, FM, FN, TM, TN>(g, acc, m0, n0, wm, wn, lane, alpha);
+  ABL_T(35);
 }
 
 // Store one tile's accumulators: alpha, bias, ReLU' mask (aux), ReLU, accumulate (beta),
 // conversion, column sums.  Lane holds C[m = mb + (lane&15)][n = nb + 4*(lane>>4) + 0..3].
 template <typename TO, int FM, int FN, int TM, int TN>
 __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&acc)[FM][FN], int m0, int n0, int wm,
-                                              int wn, int lane, float alpha) {
+                                              int wn, int lane, float alpha, int kgrp, int kgs) {
   TO* __restrict__ C = reinterpret_cast<TO*>(g.C);
   TO* __restrict__ C2 = reinterpret_cast<TO*>(g.C2);
   const bf16* __restrict__ aux = reinterpret_cast<const bf16*>(g.aux);
+  const __amdgpu_buffer_rsrc_t crs = wt_rsrc(g.C);
   const int fr = lane & 15, fq = lane >> 4;
   if constexpr (sizeof(TO) == 2) {
     if (g.ce_stats) {  // fused cross-entropy epilogue (GemmArgs::ce_stats)
@@ -422,6 +489,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&a
         const int tg = mok ? g.ce_tgt[m] : -1;
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
+          if ((i * FN + j) % kgs != kgrp) continue;  // (k-groups: another group stores it)
           const int nb = n0 + wn * TN + j * 16, n = nb + fq * 4;
           const bool nok = n < g.N;
           float v[4], mx = -INFINITY;
@@ -465,7 +533,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&a
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int m = m0 + wm * TM + i * 16 + fr;
-      if (m >= g.M) continue;
+      if (m >= g.M || (i * FN + j) % kgs != kgrp) continue;
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = alpha * acc[i][j][r] + bn[r];
@@ -492,7 +560,19 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&a
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] += o[r];
       }
-      store4<TO>(cp, v);
+      if (g.wt > 0 && !hi) {  // write-through (capgen_common.h wt_rsrc)
+        const uint32_t off = (uint32_t)(((int64_t)m * g.ldc + n) * (int64_t)sizeof(TO));
+        if constexpr (sizeof(TO) == 4) {
+          wt_store16(crs, off, wt_u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                                        __float_as_uint(v[3])});
+        } else {
+          typedef __attribute__((ext_vector_type(4))) __bf16 b4;
+          const b4 x = b4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+          wt_store8(crs, off, __builtin_bit_cast(wt_u32x2, x));
+        }
+      } else {
+        store4<TO>(cp, v);
+      }
       if (g.colsum) {  // column sums of the stored values (as rounded to TO), from registers
 #pragma unroll
         for (int r = 0; r < 4; ++r) cs[r] += (float)(TO)v[r];
@@ -519,11 +599,11 @@ __device__ __forceinline__ int xcd_slot(int bid, int nblk) {
   return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
 }
 
-template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int STAGES>
-__global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmArgs g, int tiles_n, int nblk,
-                                                                const void* zero, int splitk, float* ws,
-                                                                int* tile_cnt, int group_m, int proto) {
-  __shared__ __attribute__((aligned(1024))) char smem[TileCfg<TA, TB, BM, BN, WM, WN, STAGES>::SMEM];
+template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int STAGES, int KG = 1>
+__global__ void __launch_bounds__(64 * WM * WN * KG) gemm_bf16_kernel(GemmArgs g, int tiles_n, int nblk,
+                                                                     const void* zero, int splitk, float* ws,
+                                                                     int* tile_cnt, int group_m, int proto) {
+  __shared__ __attribute__((aligned(1024))) char smem[TileCfg<TA, TB, BM, BN, WM, WN, STAGES, KG>::SMEM];
   StampScope stamp_scope(g.stamp);
   // critical-path launch (GemmArgs::prio): beside the side streams' weight-gradient / Adam waves
   // on the same CUs, the SIMD arbiter issues this kernel's instructions first
@@ -538,7 +618,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmArgs g, int
     const int gsz = min(tiles_m - first, group_m), r = tile % per;
     mt = first + r % gsz, nt = r / gsz;
   }
-  gemm_tile<TO, TA, TB, BM, BN, WM, WN, STAGES>(g, mt, nt, tile, split, splitk, zero, ws, tile_cnt, smem, proto);
+  gemm_tile<TO, TA, TB, BM, BN, WM, WN, STAGES, KG>(g, mt, nt, tile, split, splitk, zero, ws, tile_cnt, smem, proto);
 }
 
 // Grouped launch: up to kMaxGroup independent GEMMs of one layout (e.g. every weight gradient
@@ -578,6 +658,7 @@ int g_splitk_proto = [] {
   return e ? std::atoi(e) : 0;
 }();
 std::mutex g_ws_mu;
+uint64_t* g_timing_buf = nullptr;  // ablation build, protocol bit 4096 (gemm_set_timing_buf)
 
 // make sure the stream's split-K workspace holds `bytes` (never called inside a capture)
 void ensure_ws(hipStream_t s, size_t bytes) {
@@ -604,8 +685,9 @@ Workspace get_ws(hipStream_t s) {
   return it == g_ws.end() ? Workspace{} : it->second;
 }
 
-template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int ST>
+template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int ST, int KG = 1>
 static void launch_cfg(const GemmArgs& g, hipStream_t s, int splitk) {
+  require(KG == 1 || splitk == 1, "gemm: k-group variants run without grid split-K");
   const int tn = (g.N + BN - 1) / BN, tm = (g.M + BM - 1) / BM;
   const int nblk = tn * tm * splitk;
   int dev = 0;
@@ -639,8 +721,10 @@ static void launch_cfg(const GemmArgs& g, hipStream_t s, int splitk) {
     const double per_xcd = (double)tn * tm / 8.0;
     group_m = std::max(1, std::min(tm, (int)std::lround(std::sqrt(per_xcd))));
   }
-  gemm_bf16_kernel<TO, TA, TB, BM, BN, WM, WN, ST>
-      <<<nblk, 64 * WM * WN, 0, s>>>(g, tn, nblk, g_zero_page[dev], splitk, ws, cnt, group_m, g_splitk_proto & ~8);
+  GemmArgs gk = g;
+  if ((g_splitk_proto & 4096) && g_timing_buf) gk.stamp = g_timing_buf;  // (ablation build: phase timing)
+  gemm_bf16_kernel<TO, TA, TB, BM, BN, WM, WN, ST, KG>
+      <<<nblk, 64 * WM * WN * KG, 0, s>>>(gk, tn, nblk, g_zero_page[dev], splitk, ws, cnt, group_m, g_splitk_proto & ~8);
 }
 
 // split-K workspace bound for any variant (tiles up to 256x128)
@@ -653,17 +737,24 @@ int g_variant = 0;  // experiment selector (capgen_debug_gemm_variant); 0 = tune
 // Tile / wave-grid / pipeline-depth variants.  Every variant accumulates the same K tiles
 // in the same order with the same MFMA sequence, so results are bit-identical across
 // variants: the choice is a pure speed decision (made per shape by the autotuner).
-constexpr int NVARIANTS = 22;
+constexpr int NVARIANTS = 30;
 const char* kVariantName[NVARIANTS + 1] = {"auto",        "128x128w4s3", "128x128w8s2",  "128x128w4s2",
                                            "128x64w4s2",  "64x128w4s2",  "64x64w4s2",    "64x64w4s3",
                                            "128x64w8s2",  "256x128w16s2", "128x128w16s2", "256x64w8s2",
                                            "64x64w4s4",   "64x64w4s6",   "128x64w4s4",   "64x128w4s4",
                                            "128x128w4s4", "32x64w4s2",   "64x32w4s2",    "32x32w4s2",
-                                           "64x64w8s2",   "32x64w4s3",   "64x32w4s3"};
+                                           "64x64w8s2",   "32x64w4s3",   "64x32w4s3",
+                                           // k-group variants (TileCfg KG): 'k2' = 2 k-groups of the waves named
+                                           "64x64w4k2s2", "64x64w4k2s3", "32x64w4k2s3", "64x64w4k4s2",
+                                           "32x64w4k4s2", "128x64w4k2s2", "64x128w4k2s2", "32x64w4k2s2"};
 
 // output tile width (columns) of each variant
 constexpr int kVariantBN[NVARIANTS + 1] = {0,  128, 128, 128, 64, 128, 64, 64, 64, 128, 128, 64,
-                                           64, 64,  64,  128, 128, 64, 32, 32, 64, 64,  32};
+                                           64, 64,  64,  128, 128, 64, 32, 32, 64, 64,  32,
+                                           64, 64,  64,  64,  64,  64, 128, 64};
+// k-groups of each variant (grid split-K only for KG == 1)
+constexpr int kVariantKG[NVARIANTS + 1] = {0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                           1, 1, 1, 1, 1, 1, 1, 2, 2, 2, 4, 4, 2, 2, 2};
 
 // A tile whose output row segment is narrower than a 128-B cache line shares lines of C with
 // its neighbour tile, which another workgroup -- possibly on another XCD -- writes in the same
@@ -707,6 +798,14 @@ static void launch_variant(int v, const GemmArgs& g, hipStream_t s, int sk = 1) 
     case 20: return launch_cfg<TO, TA, TB, 64, 64, 4, 2, 2>(g, s, sk);
     case 21: return launch_cfg<TO, TA, TB, 32, 64, 2, 2, 3>(g, s, sk);
     case 22: return launch_cfg<TO, TA, TB, 64, 32, 2, 2, 3>(g, s, sk);
+    case 23: return launch_cfg<TO, TA, TB, 64, 64, 2, 2, 2, 2>(g, s, sk);
+    case 24: return launch_cfg<TO, TA, TB, 64, 64, 2, 2, 3, 2>(g, s, sk);
+    case 25: return launch_cfg<TO, TA, TB, 32, 64, 2, 2, 3, 2>(g, s, sk);
+    case 26: return launch_cfg<TO, TA, TB, 64, 64, 2, 2, 2, 4>(g, s, sk);
+    case 27: return launch_cfg<TO, TA, TB, 32, 64, 2, 2, 2, 4>(g, s, sk);
+    case 28: return launch_cfg<TO, TA, TB, 128, 64, 2, 2, 2, 2>(g, s, sk);
+    case 29: return launch_cfg<TO, TA, TB, 64, 128, 2, 2, 2, 2>(g, s, sk);
+    case 30: return launch_cfg<TO, TA, TB, 32, 64, 2, 2, 2, 2>(g, s, sk);
     default: throw Error("gemm: unknown variant");
   }
 }
@@ -862,7 +961,7 @@ static Choice tune(const GemmArgs& g, hipStream_t s) {
     if (sk > max_sk || (sk > 1 && (nk < 4 * sk || !sk_ok))) break;
     if (sk > 1) ensure_ws(s, splitk_bytes(g, sk));
     for (int v = 1; v <= NVARIANTS; ++v) {
-      if (!whole_lines<TO>(v)) continue;
+      if (!whole_lines<TO>(v) || (sk > 1 && kVariantKG[v] > 1)) continue;
       const float ms = tune_time([&] { launch_variant<TO, TA, TB>(v, t, s, sk); }, s, e0, e1);
       if (ms < best_ms) best_ms = ms, best = Choice{v, sk};
     }
@@ -1073,6 +1172,12 @@ static void gemm_grouped_impl(const GemmArgs* ps, int n, DType out, bool ta, boo
   int dev = 0;
   CAPGEN_HIP(hipGetDevice(&dev));
   require(g_zero_page[dev] != nullptr, "gemm: gemm_init() not called on this device");
+  std::vector<GemmArgs> pw(ps, ps + n);  // write-through default, as gemm_bf16
+  for (auto& g : pw) {
+    if (g.wt < 0) g.wt = wt_default();
+    if ((int64_t)g.M * g.ldc * (int64_t)dsize(out) >= (int64_t)0x7FFFFFFF) g.wt = 0;
+  }
+  ps = pw.data();
   for (int i = 0; i < n; ++i) {
     const GemmArgs& g = ps[i];
     require(g.M > 0 && g.N > 0 && g.K > 0 && g.N % 4 == 0 && g.ldc % 4 == 0 && (g.aux == nullptr || g.ldaux % 4 == 0),
@@ -1161,6 +1266,7 @@ int gemm_tune_live_count() { return g_live_tuned; }
 
 void gemm_set_variant(int v) { g_variant = v; }
 void gemm_set_splitk_protocol(int p) { g_splitk_proto = p; }
+void gemm_set_timing_buf(uint64_t* p) { g_timing_buf = p; }
 void gemm_splitk_diag(int* out4, bool reset) {
   CAPGEN_HIP(hipDeviceSynchronize());
   CAPGEN_HIP(hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_sk_diag), 4 * sizeof(int)));
@@ -1204,7 +1310,10 @@ void gemm_init() {
   }
 }
 
-void gemm_bf16(const GemmArgs& g, DType out, bool ta, bool tb, hipStream_t s) {
+void gemm_bf16(const GemmArgs& g_in, DType out, bool ta, bool tb, hipStream_t s) {
+  GemmArgs g = g_in;
+  if (g.wt < 0) g.wt = wt_default();
+  if ((int64_t)g.M * g.ldc * (int64_t)dsize(out) >= (int64_t)0x7FFFFFFF) g.wt = 0;  // (32-bit buffer offsets)
   int dev = 0;
   CAPGEN_HIP(hipGetDevice(&dev));
   require(g_zero_page[dev] != nullptr, "gemm: gemm_init() not called on this device");

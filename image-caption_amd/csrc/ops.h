@@ -23,6 +23,7 @@ struct LnFwd {
   float* mean = nullptr;
   float* rstd = nullptr;
   uint64_t* stamp = nullptr;  // diagnostic timestamps (StampScope)
+  int wt = -1;                // write-through (sc1) y / v_save stores: 1/0, -1 = wt_default()
 };
 void layernorm_fwd(const LnFwd& a, DType t, hipStream_t s);
 
@@ -46,6 +47,7 @@ struct LnBwd {
   int64_t stripe_stride = 0;
   void* y_save = nullptr;  // optional: the masked output gradient dy * rowmask (T), for layernorm_param_sums
   uint64_t* stamp = nullptr;  // diagnostic timestamps (StampScope)
+  int wt = -1;                // write-through (sc1) d_res / d_a stores: 1/0, -1 = wt_default()
 };
 void layernorm_bwd(const LnBwd& a, DType t, hipStream_t s);
 // The LayerNorm parameter sums alone -- dgamma += sum y * xhat, dbeta += sum y, dbias += sum d_a --

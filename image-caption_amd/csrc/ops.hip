@@ -83,8 +83,19 @@ __global__ void __launch_bounds__(LN_THREADS) ln_fwd_kernel(LnFwd a) {
   float y[DPL];
 #pragma unroll
   for (int e = 0; e < DPL; ++e) y[e] = ((x[e] - mean) * rstd * gm[e] + bt[e]) * keep;
-  if (a.v_save) store_f<T, DPL>(reinterpret_cast<T*>(a.v_save) + base, x);
-  store_f<T, DPL>(reinterpret_cast<T*>(a.y) + base, y);
+  bool stored = false;
+  if constexpr (DPL * sizeof(T) % 16 == 0) {
+    if (a.wt > 0) {  // write-through (capgen_common.h wt_rsrc)
+      const uint32_t off = (uint32_t)(base * (int64_t)sizeof(T));
+      if (a.v_save) store_wt<T, DPL>(wt_rsrc(a.v_save), off, x);
+      store_wt<T, DPL>(wt_rsrc(a.y), off, y);
+      stored = true;
+    }
+  }
+  if (!stored) {
+    if (a.v_save) store_f<T, DPL>(reinterpret_cast<T*>(a.v_save) + base, x);
+    store_f<T, DPL>(reinterpret_cast<T*>(a.y) + base, y);
+  }
   if (lane == 0) {
     if (a.mean) a.mean[m] = mean;
     if (a.rstd) a.rstd[m] = rstd;
@@ -142,14 +153,28 @@ __global__ void __launch_bounds__(NT) ln_bwd_kernel(LnBwd a) {
       float dv[DPL];
 #pragma unroll
       for (int e = 0; e < DPL; ++e) dv[e] = rstd[u] * (g[e] - mg - xh[e] * mgx);
-      if (a.d_res) store_f<T, DPL>(reinterpret_cast<T*>(a.d_res) + base, dv);
+      constexpr bool whole = DPL * sizeof(T) % 16 == 0;
+      const bool wt = whole && a.wt > 0;
+      if (a.d_res) {
+        if constexpr (whole) {
+          if (wt) store_wt<T, DPL>(wt_rsrc(a.d_res), (uint32_t)(base * (int64_t)sizeof(T)), dv);
+          else store_f<T, DPL>(reinterpret_cast<T*>(a.d_res) + base, dv);
+        } else {
+          store_f<T, DPL>(reinterpret_cast<T*>(a.d_res) + base, dv);
+        }
+      }
       if (a.d_a) {
         if (a.drop.seed_ptr) {
 #pragma unroll
           for (int e = 0; e < DPL; ++e)
             dv[e] = drop_keep(seed, a.drop.site, (uint32_t)(base + e), a.drop.thresh) ? dv[e] * a.drop.scale : 0.f;
         }
-        store_f<T, DPL>(reinterpret_cast<T*>(a.d_a) + base, dv);
+        if constexpr (whole) {
+          if (wt) store_wt<T, DPL>(wt_rsrc(a.d_a), (uint32_t)(base * (int64_t)sizeof(T)), dv);
+          else store_f<T, DPL>(reinterpret_cast<T*>(a.d_a) + base, dv);
+        } else {
+          store_f<T, DPL>(reinterpret_cast<T*>(a.d_a) + base, dv);
+        }
 #pragma unroll
         for (int e = 0; e < DPL; ++e) dz[e] += dv[e];
       }
@@ -267,8 +292,10 @@ static void ln_fwd_dispatch(const LnFwd& a, hipStream_t s) {
     default: throw Error("layernorm: width must be 64 * {1,2,4,8,16}");
   }
 }
-void layernorm_fwd(const LnFwd& a, DType t, hipStream_t s) {
-  if (a.M <= 0 || (skip_mask() & 1)) return;
+void layernorm_fwd(const LnFwd& a_in, DType t, hipStream_t s) {
+  if (a_in.M <= 0 || (skip_mask() & 1)) return;
+  LnFwd a = a_in;
+  if (a.wt < 0) a.wt = wt_default();
   if (hz::active()) {
     using namespace hz;
     const int64_t row = a.d * (int64_t)dsize(t);
@@ -314,6 +341,7 @@ static void ln_bwd_dispatch(const LnBwd& a, hipStream_t s) {
 void layernorm_bwd(const LnBwd& a_in, DType t, hipStream_t s) {
   if (a_in.M <= 0 || (skip_mask() & 4)) return;
   LnBwd a = a_in;
+  if (a.wt < 0) a.wt = wt_default();
   if (hz::active()) {
     using namespace hz;
     const int64_t row = a.d * (int64_t)dsize(t), sb = a.d * 4, ss = std::max<int64_t>(a.stripe_stride * 4, sb);

@@ -155,6 +155,9 @@ int capgen_debug_splitk_protocol(int proto);
 /* Diagnostic: split-K hand-off counters collected under protocol bit 64 (out4[0] = tickets found
  * out of range at arrival, out4[1] = tiles combined); synchronises the device; reset != 0 zeroes. */
 int capgen_debug_splitk_diag(int* out4, int reset);
+/* Diagnostic (GEMM ablation build only, protocol bit 4096): device buffer (>= 88 u64) that block 0 of
+ * the next GEMM launches fills with per-phase s_memtime / s_memrealtime stamps (gemm_bf16.hip ABL_T). */
+int capgen_debug_gemm_timing_buf(void* dev_buf);
 /* Diagnostic: synchronous copy of an internal gradient buffer (0 tmp, 1 gOut, 2 gRes, 3 cross-K/V
  * gradient, 4-7 the last encoder block's FFN-hidden / FFN-LN / MHA-LN / QKV gradients) to host;
  * with CAPGEN_DEBUG_BWD_STOP the backward pass ends early (tools/bwd_bisect.py). */

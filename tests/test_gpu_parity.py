@@ -615,7 +615,7 @@ def test_gemm_kernel_vs_torch(in_dt, ta, tb, M, N, K):
     assert (Cd.cpu() - ref).abs().max().item() <= tol
 
 
-@pytest.mark.parametrize("variant", list(range(1, 23)) + [206, 303, 403, 612, 813, 1314, 217, 319, 420])
+@pytest.mark.parametrize("variant", list(range(1, 31)) + [206, 303, 403, 612, 813, 1314, 217, 319, 420])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 1)])
 def test_gemm_every_variant_and_splitk(variant, ta, tb):
     """Each tile/wave/stage variant (and split-K factor: variant + 100*splitk) computes the
@@ -646,7 +646,7 @@ def test_gemm_every_variant_and_splitk(variant, ta, tb):
         _lib.check(lib.capgen_debug_gemm_variant(0))
 
 
-@pytest.mark.parametrize("variant", [0, 6, 17, 303, 813])
+@pytest.mark.parametrize("variant", [0, 6, 17, 303, 813, 23, 26, 27])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("K", [72, 1000])
 def test_gemm_k_tail_never_reads_past_the_operands(variant, ta, tb, K):
@@ -682,6 +682,40 @@ def test_gemm_k_tail_never_reads_past_the_operands(variant, ta, tb, K):
     out = Cd.cpu()
     assert torch.isfinite(out).all(), int((~torch.isfinite(out)).sum())
     assert (out - ref).abs().max().item() <= 2e-3 * np.sqrt(K)
+
+
+@pytest.mark.parametrize("kg,split", [(23, 206), (24, 207), (26, 406), (25, 221), (27, 417), (28, 204), (29, 205),
+                                      (30, 217)])
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 1)])
+def test_gemm_k_groups_equal_grid_split_k_bitwise(kg, split, ta, tb):
+    """A k-group variant (TileCfg KG: KG wave groups of one workgroup run contiguous k-chunks and
+    sum their partial tiles through LDS in group order) equals the same tile with grid split-K =
+    KG (slices summed in slice order) bit for bit -- f32 and bf16 outputs, K tails included."""
+    import ctypes as C
+    from capgen import _lib
+    lib = _lib.load()
+    M, N, K = 304, 328, 1480
+    g = torch.Generator(device="cpu").manual_seed(kg * 7 + ta)
+    A = torch.randn(M, K, generator=g).bfloat16()
+    Bm = torch.randn(N, K, generator=g).bfloat16()
+    Ad = (A.t().contiguous() if ta else A).to(DEV)
+    Bd = (Bm.t().contiguous() if tb else Bm).to(DEV)
+    outs = {}
+    for odt, code in ((torch.float32, 0), (torch.bfloat16, 1)):
+        for v in (kg, split):
+            Cd = torch.full((M, N), float("nan"), dtype=odt, device=DEV)
+            _lib.check(lib.capgen_debug_gemm_variant(v))
+            try:
+                _lib.check(lib.capgen_debug_gemm(M, N, K, C.c_void_p(Ad.data_ptr()), M if ta else K, ta,
+                                                 C.c_void_p(Bd.data_ptr()), N if tb else K, tb, C.c_void_p(Cd.data_ptr()),
+                                                 N, 1, code, None, 1.0, 0, 0, None))
+                torch.cuda.synchronize()
+            finally:
+                _lib.check(lib.capgen_debug_gemm_variant(0))
+            outs[(code, v)] = Cd.cpu()
+        assert torch.equal(outs[(code, kg)], outs[(code, split)]), (odt, kg, split)
+    ref = A.float() @ Bm.float().t()
+    assert (outs[(0, kg)] - ref).abs().max().item() <= 2e-3 * np.sqrt(K)
 
 
 def test_splitk_combine_bit_reproducible_under_load():
