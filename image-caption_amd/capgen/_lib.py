@@ -71,6 +71,8 @@ _SIGS = {
     "capgen_debug_gemm": (C.c_int, [C.c_int, C.c_int, C.c_int, _P, C.c_int64, C.c_int, _P, C.c_int64, C.c_int,
                                     _P, C.c_int64, C.c_int, C.c_int, _P, C.c_float, C.c_int, C.c_int, _P]),
     "capgen_debug_gemm_variant": (C.c_int, [C.c_int]),
+    "capgen_debug_ffn_persist": (C.c_int, [C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, C.c_int, C.c_int, _P]),
+    "capgen_debug_persist_giveups": (C.c_int, [C.c_int, _P]),
     "capgen_debug_splitk_protocol": (C.c_int, [C.c_int]),
     "capgen_debug_splitk_diag": (C.c_int, [_P, C.c_int]),
     "capgen_debug_gemm_timing_buf": (C.c_int, [_P]),

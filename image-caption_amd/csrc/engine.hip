@@ -27,6 +27,7 @@
 #include "gemm.h"
 #include "hazard.h"
 #include "layout.h"
+#include "persist.h"
 #include "ops.h"
 #include "variants.h"
 #include "rl.h"
@@ -1127,6 +1128,31 @@ struct capgen_engine {
     if (side) col_pending.push_back(ColJob{gH, M, f, GS(b1)});                           // db1 = colsum
     dw_side(gH, f, X, d, W1, d, M, f, d, nullptr, s);
     linear_dx(gH, f, W1, d, lb.d_res, d, M, f, d, 1, nullptr, nullptr, s);
+    flush_deferred(s);
+  }
+  // Deferred block flush (CAPGEN_FLUSH_DEFER, experiment): a transformer block's weight-gradient
+  // group and bucket update are issued after the NEXT block's FFN input gradients instead of at the
+  // block's end, so the side stream's largest launch (the block's grouped dW, 64 KB LDS and 16
+  // waves per CU) overlaps the latency-bound LayerNorm / attention / projection kernels rather than
+  // the FFN-down input gradient, the GEMM it slowed most (un-profiled timeline: 2304x2048x512 dX
+  // 29-39 us beside the group vs 13.4 us alone)
+  // Measured neutral (3-round A/B 3.048-3.067 vs 3.046-3.067 ms/step): the contention moves to the
+  // kernels the group then overlaps.  Off; CAPGEN_FLUSH_DEFER=1 enables.
+  bool flush_defer = [] {
+    const char* e = std::getenv("CAPGEN_FLUSH_DEFER");
+    return e && e[0] == '1';
+  }();
+  bool deferred = false;
+  int64_t deferred_off = 0, deferred_n = 0;
+  void defer_bucket(int64_t off, int64_t n, hipStream_t s) {
+    flush_deferred(s);
+    if (!flush_defer || es2 == s) return bucket(off, n, s);
+    deferred = true, deferred_off = off, deferred_n = n;
+  }
+  void flush_deferred(hipStream_t s) {
+    if (!deferred) return;
+    deferred = false;
+    bucket(deferred_off, deferred_n, s);
   }
   // MHA output projection + LayerNorm backward: lb as above (d_res = grad wrt the residual /
   // query input); writes grad wrt the attention output into gATT.
@@ -1305,6 +1331,7 @@ struct capgen_engine {
     require(fB > 0, "backward: call forward first");
     grads_sharded = false;
     stamp_next = stamp_fwd_end;
+    deferred = false;  // (a diagnostic early return may have left one)
     const int B = fB, N = fN, Lq = fT - 1, Me = B * N, Md = B * Lq, d = L.d, dd = L.dd;
     const int He = L.He, Hd = L.Hd, dke = d / He, dkd = dd / Hd;
     const bool on = fwd_drop;
@@ -1424,7 +1451,8 @@ struct capgen_engine {
       dw_side(gb.gQKV, 3 * dd, a.D[l], dd, w.Wqkv, dd, Md, 3 * dd, dd, nullptr, hs);
       linear_dx(gb.gQKV, 3 * dd, w.Wqkv, dd, gR, dd, Md, 3 * dd, dd, 1, nullptr, nullptr, hs);
       if (l % bucket_blocks == 0)  // blocks l .. l + bucket_blocks - 1 (contiguous in the arena)
-        bucket(w.Wqkv, dec_end(std::min(l + bucket_blocks - 1, L.Ld - 1)) - w.Wqkv, hs);
+        (ov || l == 0 ? bucket(w.Wqkv, dec_end(std::min(l + bucket_blocks - 1, L.Ld - 1)) - w.Wqkv, hs)
+                      : defer_bucket(w.Wqkv, dec_end(std::min(l + bucket_blocks - 1, L.Ld - 1)) - w.Wqkv, hs));
       if (ov) dec0_on_side = true;
       std::swap(gO, gR);  // gO = grad wrt D_l
     }
@@ -1473,7 +1501,9 @@ struct capgen_engine {
       const auto& w = L.enc[l];
       enc_layer_bwd(w, a.enc[l], a.genc[l], a.X[l], B, N, cfg.encode_mask ? a.valid : nullptr, l, on, gO, gR, s);
       if (dbg_stop >= 2 && l == L.Le - 1) return join(s);  // 3, 4: after the whole block
-      if (l % bucket_blocks == 0) bucket(w.Wqkv, enc_end(std::min(l + bucket_blocks - 1, L.Le - 1)) - w.Wqkv, s);
+      if (l % bucket_blocks == 0)
+        (l == 0 ? bucket(w.Wqkv, enc_end(std::min(l + bucket_blocks - 1, L.Le - 1)) - w.Wqkv, s)
+                : defer_bucket(w.Wqkv, enc_end(std::min(l + bucket_blocks - 1, L.Le - 1)) - w.Wqkv, s));
     }
     // the tail of the step's dependency chain: the encoder-embedding LayerNorm backward and
     // weight gradient, then its Adam, which the next forward's first GEMM needs -- on the
@@ -2367,6 +2397,21 @@ int capgen_debug_attention(int dtype, int B, int H, int Lq, int Lk, int dk, cons
 
 int capgen_debug_gemm_variant(int v) {
   return guarded([&] { gemm_set_variant(v); });
+}
+
+int capgen_debug_ffn_persist(int M, int d, int fe, const void* X, const void* W1, const float* b1, const void* W2,
+                             void* H, void* Y, int grid, int acquire, void* stream) {
+  return guarded([&] {
+    gemm_init();
+    GemmArgs g1, g2;
+    g1.M = M, g1.N = fe, g1.K = d, g1.A = X, g1.lda = d, g1.B = W1, g1.ldb = d, g1.C = H, g1.ldc = fe, g1.bias = b1;
+    g2.M = M, g2.N = d, g2.K = fe, g2.A = H, g2.lda = fe, g2.B = W2, g2.ldb = fe, g2.C = Y, g2.ldc = d;
+    ffn_persistent(g1, g2, grid, acquire, (hipStream_t)stream);
+  });
+}
+
+int capgen_debug_persist_giveups(int reset, int* out) {
+  return guarded([&] { *out = ffn_persistent_giveups(reset != 0); });
 }
 
 int capgen_debug_copy_buffer(capgen_t* h, int which, void* host_dst, int64_t bytes) {

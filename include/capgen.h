@@ -145,6 +145,13 @@ int capgen_debug_gemm(int M, int N, int K, const void* A, int64_t lda, int ta, c
 
 /* Experiment hook: force a GEMM tile/wave/pipeline variant (0 = production heuristic). */
 int capgen_debug_gemm_variant(int variant);
+/* Experiment (persist.hip): the FFN pair H = relu(X.W1^T + b1) [M, fe], Y = H.W2^T [M, d] (bf16,
+ * weights [out][in]) as ONE persistent launch of `grid` workgroups with row-block dependency
+ * counters; acquire = 0 drops the consumer's agent acquire (diagnostic). */
+int capgen_debug_ffn_persist(int M, int d, int fe, const void* X, const void* W1, const float* b1, const void* W2,
+                             void* H, void* Y, int grid, int acquire, void* stream);
+/* Persistent-launch spins that gave up (0 in a correct run); synchronises; reset != 0 zeroes. */
+int capgen_debug_persist_giveups(int reset, int* out);
 /* Diagnostic hook: the in-launch split-K combine's hand-off protocol (0 = the production form:
  * sc1 slab stores, agent acquire + plain slab loads in the combining workgroup, tickets re-armed
  * by the last arriver's atomic exchange).  Bits: 1 adds a writer release fence, 2 drops the

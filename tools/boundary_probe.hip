@@ -32,6 +32,11 @@ __global__ void __launch_bounds__(256) k(Args<BYTES> a) {
   if (threadIdx.x == 0 && blockIdx.x == 0) a.out[0] += (LDS > 0 ? sm[5] : 1.f);
 }
 
+__global__ void spin_kernel(long long cycles) {
+  const long long t0 = clock64();
+  while (clock64() - t0 < cycles) __builtin_amdgcn_s_sleep(8);
+}
+
 template <int BYTES, int LDS>
 int run(hipStream_t s, float* out, int blocks, const char* name) {
   Args<BYTES> a{};
@@ -48,6 +53,14 @@ int run(hipStream_t s, float* out, int blocks, const char* name) {
   CK(hipEventSynchronize(e1));
   float ms_e = 0;
   CK(hipEventElapsedTime(&ms_e, e0, e1));
+  // the same chain queued behind a 20 ms spin: the host is far ahead, so this is the GPU-side price
+  spin_kernel<<<1, 64, 0, s>>>(20LL * 2100 * 1000);
+  CK(hipEventRecord(e0, s));
+  for (int i = 0; i < n; ++i) k<BYTES, LDS><<<blocks, 256, 0, s>>>(a);
+  CK(hipEventRecord(e1, s));
+  CK(hipEventSynchronize(e1));
+  float ms_q = 0;
+  CK(hipEventElapsedTime(&ms_q, e0, e1));
   hipGraph_t g;
   hipGraphExec_t ge;
   CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
@@ -62,8 +75,8 @@ int run(hipStream_t s, float* out, int blocks, const char* name) {
   CK(hipEventSynchronize(e1));
   float ms_g = 0;
   CK(hipEventElapsedTime(&ms_g, e0, e1));
-  std::printf("%-28s blocks %4d  eager %6.2f us/launch  graph %6.2f us/launch\n", name, blocks, ms_e * 1e3 / n,
-              ms_g * 1e3 / (5 * n));
+  std::printf("%-28s blocks %4d  eager %6.2f  eager-queued %6.2f  graph %6.2f us/launch\n", name, blocks,
+              ms_e * 1e3 / n, ms_q * 1e3 / n, ms_g * 1e3 / (5 * n));
   CK(hipGraphExecDestroy(ge));
   CK(hipGraphDestroy(g));
   return 0;

@@ -2,7 +2,7 @@
 split-K, against the tuned choice (capgen/tune_gfx950.txt).  The per-workgroup k-loop is latency-bound
 (tools/gemm_kstep_sweep.py: time independent of M), so split-K is the lever for K-deep shapes.
 
-  python tools/gemm_splitk_sweep.py [--cold]
+  python tools/gemm_splitk_sweep.py [--variants 1,7 --splits 1 --out x.json]
 """
 import argparse
 import ctypes as C
@@ -35,7 +35,12 @@ SPLITS = [1, 2, 3, 4, 6, 8]
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--variants", default=",".join(map(str, VARIANTS)))
+    ap.add_argument("--splits", default=",".join(map(str, SPLITS)))
+    ap.add_argument("--out", default="gemm_splitk_sweep.json")
     args = ap.parse_args()
+    variants = [int(v) for v in args.variants.split(",") if v]
+    splits = [int(v) for v in args.splits.split(",") if v]
     lib = _lib.load()
     dev = torch.device("cuda", 0)
     out = []
@@ -72,8 +77,8 @@ def main():
         _lib.check(lib.capgen_debug_gemm_variant(0))
         row["tuned_us"] = round(graph_time(), 2)
         best = (1e9, None)
-        for v in VARIANTS:
-            for sk in SPLITS:
+        for v in variants:
+            for sk in splits:
                 if sk > 1 and ((K + 63) // 64 < 2 * sk or v >= 23):  # (k-group variants: no grid split-K)
                     continue
                 _lib.check(lib.capgen_debug_gemm_variant(v + 100 * sk))
@@ -87,9 +92,10 @@ def main():
         _lib.check(lib.capgen_debug_gemm_variant(0))
         row["best"] = best[1]
         row["best_us"] = round(best[0], 2)
-        print(json.dumps({k: row[k] for k in ("shape", "gflop", "tuned_us", "best", "best_us")}), flush=True)
+        print(json.dumps({k: row[k] for k in ("shape", "gflop", "tuned_us", "best", "best_us")} if len(row) > 8 else row),
+              flush=True)
         out.append(row)
-    with open(os.path.join(REPO, "gpurun_out", "gemm_splitk_sweep.json"), "w") as fh:
+    with open(os.path.join(REPO, "gpurun_out", args.out), "w") as fh:
         json.dump(out, fh, indent=1)
 
 

@@ -1,0 +1,109 @@
+"""Persistent FFN pair (csrc/persist.hip) against the two plain launches it replaces, at the C2 encoder
+and decoder FFN shapes: bit-identity with the same tile variant (64x64w4s3, forced), agreement with
+torch, and GPU time under hipGraph replay (no host launch cost) for the persistent grid sizes, the
+same-variant pair and the autotuned pair.
+
+  python tools/persist_ffn.py [--reps 20]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "image-caption_amd"))
+import torch  # noqa: E402
+
+from capgen import _lib  # noqa: E402
+
+V7 = 7  # 64x64w4s3: the persistent kernel's tile
+
+
+def ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    lib = _lib.load()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    out = []
+    for name, M, d, fe in (("enc FFN", 2304, 512, 2048), ("dec FFN", 1216, 512, 2048)):
+        X = (torch.randn(M, d, device=dev) * 0.5).to(torch.bfloat16)
+        W1 = (torch.randn(fe, d, device=dev) / d ** 0.5).to(torch.bfloat16)
+        b1 = torch.randn(fe, device=dev) * 0.1
+        W2 = (torch.randn(d, fe, device=dev) / fe ** 0.5).to(torch.bfloat16)
+        H = torch.empty(M, fe, device=dev, dtype=torch.bfloat16)
+        Y = torch.empty(M, d, device=dev, dtype=torch.bfloat16)
+        Hr, Yr = torch.empty_like(H), torch.empty_like(Y)
+        s = torch.cuda.Stream(dev)
+
+        def pair(Ho, Yo):
+            _lib.check(lib.capgen_debug_gemm(M, fe, d, ptr(X), d, 0, ptr(W1), d, 0, ptr(Ho), fe, 1, 1, ptr(b1), 1.0, 0, 1,
+                                             C.c_void_p(s.cuda_stream)))
+            _lib.check(lib.capgen_debug_gemm(M, d, fe, ptr(Ho), fe, 0, ptr(W2), fe, 0, ptr(Yo), d, 1, 1, None, 1.0, 0, 0,
+                                             C.c_void_p(s.cuda_stream)))
+
+        def persist(grid, acq):
+            _lib.check(lib.capgen_debug_ffn_persist(M, d, fe, ptr(X), ptr(W1), ptr(b1), ptr(W2), ptr(H), ptr(Y), grid, acq,
+                                                    C.c_void_p(s.cuda_stream)))
+
+        def gtime(fn):
+            with torch.cuda.stream(s):
+                fn()
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    for _ in range(args.reps):
+                        fn()
+                g.replay()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                for _ in range(3):
+                    g.replay()
+                e1.record(s)
+                e1.synchronize()
+                return round(e0.elapsed_time(e1) / (3 * args.reps) * 1e3, 2)
+
+        row = {"shape": name, "M": M, "d": d, "fe": fe}
+        _lib.check(lib.capgen_debug_gemm_variant(V7))
+        with torch.cuda.stream(s):
+            pair(Hr, Yr)
+        torch.cuda.synchronize()
+        ref = torch.relu(X.float() @ W1.float().t() + b1).to(torch.bfloat16)
+        row["pair_vs_torch_H_maxabs"] = float((Hr.float() - ref.float()).abs().max())
+        exact = True
+        for grid in (256, 512, 768):
+            for rep in range(3):
+                H.fill_(float("nan"))
+                Y.fill_(float("nan"))
+                with torch.cuda.stream(s):
+                    persist(grid, 1)
+                torch.cuda.synchronize()
+                exact &= bool(torch.equal(H, Hr)) and bool(torch.equal(Y, Yr))
+        gv = C.c_int(0)
+        _lib.check(lib.capgen_debug_persist_giveups(1, C.byref(gv)))
+        row["persist_bit_identical_to_pair"] = exact
+        row["giveups"] = gv.value
+        row["pair_v7_us"] = gtime(lambda: pair(Hr, Yr))
+        for grid in (256, 512, 768):
+            row[f"persist_g{grid}_us"] = gtime(lambda: persist(grid, 1))
+        row["persist_g512_noacquire_us(diag)"] = gtime(lambda: persist(512, 0))
+        _lib.check(lib.capgen_debug_gemm_variant(0))
+        row["pair_tuned_us"] = gtime(lambda: pair(Hr, Yr))
+        _lib.check(lib.capgen_debug_persist_giveups(1, C.byref(gv)))
+        row["giveups_after_timing"] = gv.value
+        print(json.dumps(row), flush=True)
+        out.append(row)
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(REPO, "gpurun_out", "persist_ffn.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
