@@ -124,6 +124,7 @@ struct GenWS {
   int R = 0, N = 0;  // capacity (rows, regions)
   void *x, *x1, *x2, *q, *att, *tmp, *h, *E;
   float *mean, *rstd, *Pc, *logits;
+  float2* dstats;         // bf16 decode: classifier slab stats [R][ceil(V/16)] (GemmArgs::dec_stats)
   float* cand_v;          // beam: each row's k finalists (beam_step_topk)
   int32_t* cand_i;
   void* cache;            // [Ld][R][Tcap][2d]: row r's K/V of position t at [l][r][t]
@@ -1796,6 +1797,7 @@ struct capgen_engine {
     p.take(g.rstd, R);
     p.take(g.Pc, (size_t)R * L.Hd * N);
     p.take(g.logits, (size_t)R * L.V);
+    p.take(g.dstats, (size_t)R * ((L.V + 15) / 16));
     p.take(g.cand_v, (size_t)R * 16);
     p.take(g.cand_i, (size_t)R * 16);
     T_(g.cache, (int64_t)L.Ld * R * Tc * 2 * dd);
@@ -1898,8 +1900,24 @@ struct capgen_engine {
       move_first_fwd(g.x, a.X[L.Le], R, 1, Bimg, N, g.x2, g.h, g.tmp, g.x1, nullptr, nullptr, nullptr, false, s);
       xo = g.x1;
     }
-    linear(xo, dd, L.Wc, dd, g.logits, L.V, DType::F32, R, L.V, dd, P(L.bc), 0, s);
+    if (slab_decode()) {  // f32 logits + per-16-column-slab {max, exp-sum} for the selection
+      GemmArgs ga;
+      ga.M = R, ga.N = L.V, ga.K = dd, ga.A = xo, ga.lda = dd, ga.B = W(L.Wc), ga.ldb = dd;
+      ga.C = g.logits, ga.ldc = L.V, ga.bias = P(L.bc);
+      ga.dec_stats = g.dstats, ga.dec_ld = (L.V + 15) / 16;
+      if (stamp_on) ga.stamp = stamp(s, "gemm NT " + dims(R, L.V, dd) + " classifier+slab stats");
+      gemm(ga, act, DType::F32, false, false, s);
+    } else {
+      linear(xo, dd, L.Wc, dd, g.logits, L.V, DType::F32, R, L.V, dd, P(L.bc), 0, s);
+    }
   }
+  // bf16 decode: the classifier epilogue writes slab stats and the greedy / beam selection reads
+  // k * 16 logits per row instead of the whole row (CAPGEN_SLAB_DECODE=0: full-row kernels)
+  bool slab_decode_on = [] {
+    const char* e = std::getenv("CAPGEN_SLAB_DECODE");
+    return !(e && e[0] == '0');
+  }();
+  bool slab_decode() const { return slab_decode_on && act == DType::BF16 && L.V % 4 == 0 && slab_select_ok(L.V); }
 
   void greedy(const void* feats, DType ft, const float* pos, int B, int N, int64_t* ids_out, float* attn_out,
               hipStream_t s) {
@@ -1924,7 +1942,10 @@ struct capgen_engine {
     for (int t = 0; t < L.maxlen - 1; ++t) {
       dec_step(B, B, N, t, g.cache, g.ids, attn_out != nullptr, s);
       if (attn_out) attention_head_mean(g.Pc, B, L.Hd, 1, N, 0, attn_out + (int64_t)t * B * N, s);
-      argmax_softmax(g.logits, B, L.V, ids_out, W, t + 1, g.ids + t + 1, Tc, s, decode_logsm);
+      if (slab_decode())  // argmax of the logits = argmax of the (log-)softmax
+        slab_argmax(g.logits, g.dstats, B, L.V, ids_out, W, t + 1, g.ids + t + 1, Tc, s);
+      else
+        argmax_softmax(g.logits, B, L.V, ids_out, W, t + 1, g.ids + t + 1, Tc, s, decode_logsm);
     }
   }
 
@@ -1947,7 +1968,11 @@ struct capgen_engine {
     // position 0: every beam holds <START>; top-k of beam 0's distribution (model.py:148-166)
     beam_kvrow_kernel<<<(R * Tc + 255) / 256, 256, 0, s>>>(g.kvrow2, g.kvrow, Tc, -1, g.ids, B, R);  // [r][0] = r
     dec_step(R, B, N, 0, g.cache, g.ids, false, s);
-    beam_step_topk(g.logits, nullptr, 1, B, L.V, k, decode_logsm, g.cand_v, g.cand_i, g.bprob, g.bsrc, g.btok, s);
+    if (slab_decode())
+      beam_step_topk_slab(g.logits, g.dstats, nullptr, 1, B, L.V, k, decode_logsm, g.cand_v, g.cand_i, g.bprob, g.bsrc,
+                          g.btok, s);
+    else
+      beam_step_topk(g.logits, nullptr, 1, B, L.V, k, decode_logsm, g.cand_v, g.cand_i, g.bprob, g.bsrc, g.btok, s);
     CAPGEN_HIP(hipMemsetAsync(g.bsrc, 0, sizeof(int32_t) * R, s));  // all beams descend from beam 0 at t = 0
     // The K/V cache is never copied: row r writes its position-t K/V at [l][r][t] and reads
     // position j of its history from row kvrow[r][j] (the beam it descended from there); a
@@ -1966,7 +1991,12 @@ struct capgen_engine {
     reorder(0);
     for (int t = 1; t < Tw - 1; ++t) {
       dec_step(R, B, N, t, g.cache, g.ids, false, s, g.kvrow);
-      beam_step_topk(g.logits, g.bprob, k, B, L.V, k, decode_logsm, g.cand_v, g.cand_i, g.bprob2, g.bsrc, g.btok, s);
+      if (slab_decode())
+        beam_step_topk_slab(g.logits, g.dstats, g.bprob, k, B, L.V, k, decode_logsm, g.cand_v, g.cand_i, g.bprob2,
+                            g.bsrc, g.btok, s);
+      else
+        beam_step_topk(g.logits, g.bprob, k, B, L.V, k, decode_logsm, g.cand_v, g.cand_i, g.bprob2, g.bsrc, g.btok,
+                       s);
       std::swap(g.bprob, g.bprob2);
       reorder(t);
     }

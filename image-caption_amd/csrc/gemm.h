@@ -40,6 +40,11 @@ struct GemmArgs {
   int64_t ce_ld = 0;
   const int32_t* ce_tgt = nullptr;
   float* ce_tlogit = nullptr;
+  // decode classifier epilogue (bf16 operands, f32 out): C[m][n] = v = alpha * acc + bias as usual,
+  // plus dec_stats[m * dec_ld + c] = {max, sum exp(v - max)} of each 16-column slab c -- the
+  // beam / greedy selection then reads 1/8 of the row (ops.hip slab_topk / slab_argmax)
+  float2* dec_stats = nullptr;
+  int64_t dec_ld = 0;
   uint64_t* stamp = nullptr;  // diagnostic timestamps (capgen_common.h StampScope); grouped: p[0]'s
   int wt = -1;                // write-through (sc1) C stores (bf16 path): 1/0, -1 = wt_default()
 };

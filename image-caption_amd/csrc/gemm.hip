@@ -230,6 +230,7 @@ void gemm_hz_regions(const GemmArgs& g, DType in, DType out, bool ta, bool tb, s
   v.push_back(rd(g.alpha_ptr, 4));
   v.push_back(blk(g.colsum, g.colsum_stripes, g.N * 4, g.colsum_stride * 4, ACC));
   v.push_back(blk(g.ce_stats, g.M, (int64_t)((g.N + 15) / 16) * 8, g.ce_ld * 8, WR));
+  v.push_back(blk(g.dec_stats, g.M, (int64_t)((g.N + 15) / 16) * 8, g.dec_ld * 8, WR));
   v.push_back(rd(g.ce_tgt, (int64_t)g.M * 4));
   v.push_back(wr(g.ce_tlogit, (int64_t)g.M * 4));
 }
@@ -261,6 +262,7 @@ static void gemm_impl(const GemmArgs& g, DType in, DType out, bool ta, bool tb, 
   require(g.K > 0, "gemm: K must be positive");
   require(!g.colsum || !g.beta, "gemm: colsum requires beta == 0");
   require(!g.cin || in == DType::BF16, "gemm: cin is a bf16-path epilogue input");
+  require(!g.dec_stats || in == DType::BF16, "gemm: dec_stats is a bf16-path epilogue output");
   require(!g.C2 || (in == DType::BF16 && g.nsplit % 4 == 0 && !g.beta && !g.colsum),
           "gemm: a split output (C2) needs the bf16 path, nsplit % 4 == 0, no beta / colsum");
   if (hz::active()) {

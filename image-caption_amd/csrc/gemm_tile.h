@@ -522,6 +522,40 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&a
       return;
     }
   }
+  if constexpr (sizeof(TO) == 4) {
+    if (g.dec_stats) {  // decode classifier epilogue (GemmArgs::dec_stats): f32 logits + slab stats
+      // same fragment geometry as the cross-entropy epilogue above: the 4 lane groups of a row hold
+      // its 16-column slab, so the slab max / exp-sum are two xor-shuffles
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int m = m0 + wm * TM + i * 16 + fr;
+        const bool mok = m < g.M;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          if ((i * FN + j) % kgs != kgrp) continue;
+          const int nb = n0 + wn * TN + j * 16, n = nb + fq * 4;
+          const bool nok = n < g.N;
+          float v[4], mx = -INFINITY;
+          if (nok) {
+            const float4 b4 = g.bias ? *reinterpret_cast<const float4*>(g.bias + n) : float4{0.f, 0.f, 0.f, 0.f};
+            v[0] = alpha * acc[i][j][0] + b4.x, v[1] = alpha * acc[i][j][1] + b4.y;
+            v[2] = alpha * acc[i][j][2] + b4.z, v[3] = alpha * acc[i][j][3] + b4.w;
+            mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+          }
+          mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+          mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+          float sum = 0.f;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sum += nok ? __expf(v[r] - mx) : 0.f;
+          sum += __shfl_xor(sum, 16, 64);
+          sum += __shfl_xor(sum, 32, 64);
+          if (mok && nok) store4<TO>(C + (int64_t)m * g.ldc + n, v);
+          if (mok && fq == 0 && nb < g.N) g.dec_stats[(int64_t)m * g.dec_ld + nb / 16] = float2{mx, sum};
+        }
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int n = n0 + wn * TN + j * 16 + fq * 4;

@@ -103,6 +103,18 @@ void argmax_softmax(const float* logits, int B, int V, int64_t* ids_out, int64_t
 // out_prob/src/tok[sel*B + i]; cand_v/cand_i: k_in*B*k scratch (each row's k finalists)
 void beam_step_topk(const float* logits, const float* prev, int k_in, int B, int V, int k, int logsm, float* cand_v,
                     int32_t* cand_i, float* out_prob, int32_t* out_src, int32_t* out_tok, hipStream_t s);
+// bf16 decode selection from the classifier epilogue's slab stats (GemmArgs::dec_stats: {max,
+// sum exp(v - max)} per row and 16-column slab, stats row stride S = ceil(V / 16)):
+// greedy -- argmax of the logits (first index on ties), read from the best slab only;
+// beam -- each row's k best scores from its k best slabs (every top-k element lies in the k
+// slabs with the largest maxima under (max desc, slab asc)), then the per-image merge.
+// V <= 16384 (S <= 1024 slabs, 16 per lane in registers).
+bool slab_select_ok(int V);
+void slab_argmax(const float* logits, const float2* stats, int B, int V, int64_t* ids_out, int64_t ids_ld, int col,
+                 int32_t* next_ids, int64_t next_ld, hipStream_t s);
+void beam_step_topk_slab(const float* logits, const float2* stats, const float* prev, int k_in, int B, int V, int k,
+                         int logsm, float* cand_v, int32_t* cand_i, float* out_prob, int32_t* out_src,
+                         int32_t* out_tok, hipStream_t s);
 void bump_seed(uint64_t* seed, hipStream_t s);
 
 }  // namespace capgen

@@ -1209,6 +1209,154 @@ void beam_step_topk(const float* logits, const float* prev, int k_in, int B, int
   CAPGEN_HIP(hipGetLastError());
 }
 
+// ---- bf16 decode selection from slab stats (GemmArgs::dec_stats) ----------------------------
+// One wave per row, 4 rows per workgroup.  The row's ceil(V/16) slab stats (8 B each, 1/8 of the
+// f32 logits) sit NS per lane in registers: one pass gives the row max M and the exp-sum
+// se = sum_c s_c exp(m_c - M) (the softmax of the selected elements is exp(x - M) / se), and each
+// lane's sorted best slabs.  Any element of the row's top k (value desc, index asc) lies in one of
+// the k best slabs under (max desc, slab asc): every slab ranked before the slab of the k-th best
+// element holds, as its maximum, a distinct element ranked before it.  So only k * 16 logits are
+// read back.  (The softmax is monotone in the logit; two logits rounding to one probability could
+// order by index differently than a full scan would -- the bf16 path is held to the fp32 engine by
+// the top-2-margin tests, the fp32 parity path keeps the exact full-row kernels above.)
+constexpr int kSlabNS = 16;  // slabs per lane: V <= 64 * 16 * 16 = 16384
+bool slab_select_ok(int V) { return V >= 1 && (V + 15) / 16 <= 64 * kSlabNS; }
+
+struct SlabRow {
+  float M, se;
+};
+// the row max and exp-sum from the stats; every lane ends with both
+__device__ __forceinline__ SlabRow slab_row_stats(const float2* __restrict__ st, int S, int lane, float (&mx)[kSlabNS]) {
+  float2 x[kSlabNS];
+  float M = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < kSlabNS; ++u) {
+    const int c = lane + 64 * u;
+    x[u] = c < S ? st[c] : float2{-INFINITY, 0.f};
+    mx[u] = x[u].x;
+    M = fmaxf(M, x[u].x);
+  }
+  M = wave_max(M);
+  float se = 0.f;
+#pragma unroll
+  for (int u = 0; u < kSlabNS; ++u)
+    if (lane + 64 * u < S) se += x[u].y * __expf(x[u].x - M);
+  return SlabRow{M, wave_sum(se)};
+}
+
+__global__ void __launch_bounds__(256) slab_argmax_kernel(const float* __restrict__ logits,
+                                                          const float2* __restrict__ stats, int B, int V,
+                                                          int64_t* __restrict__ ids_out, int64_t ids_ld, int col,
+                                                          int32_t* __restrict__ next_ids, int64_t next_ld) {
+  const int lane = threadIdx.x & 63, b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;  // (whole waves)
+  const int S = (V + 15) / 16;
+  const float2* st = stats + (int64_t)b * S;
+  // best slab of this lane (max desc, slab asc), then of the wave
+  float best = -INFINITY;
+  int bidx = 0x7fffffff, bpos = lane;
+#pragma unroll
+  for (int u = 0; u < kSlabNS; ++u) {
+    const int c = lane + 64 * u;
+    if (c < S) {
+      const float m = st[c].x;
+      if (m > best) best = m, bidx = c;  // c ascends: ties keep the first
+    }
+  }
+  wave_best(best, bidx, bpos);
+  // the slab's 16 logits: the first column holding the maximum
+  const int c = bidx * 16 + lane;
+  float v = -INFINITY;
+  int vi = 0x7fffffff, vp = lane;
+  if (lane < 16 && c < V) v = logits[(int64_t)b * V + c], vi = c;
+  wave_best(v, vi, vp);
+  if (lane == 0) {
+    ids_out[(int64_t)b * ids_ld + col] = vi;
+    if (next_ids) next_ids[(int64_t)b * next_ld] = vi;
+  }
+}
+void slab_argmax(const float* logits, const float2* stats, int B, int V, int64_t* ids_out, int64_t ids_ld, int col,
+                 int32_t* next_ids, int64_t next_ld, hipStream_t s) {
+  require(slab_select_ok(V), "slab_argmax: V must be in [1, 16384]");
+  slab_argmax_kernel<<<(B + 3) / 4, 256, 0, s>>>(logits, stats, B, V, ids_out, ids_ld, col, next_ids, next_ld);
+  CAPGEN_HIP(hipGetLastError());
+}
+
+template <int KM>
+__global__ void __launch_bounds__(256) slab_row_topk_kernel(const float* __restrict__ logits,
+                                                            const float2* __restrict__ stats,
+                                                            const float* __restrict__ prev, int rows, int B, int V,
+                                                            int k, int logsm, float* __restrict__ cand_v,
+                                                            int* __restrict__ cand_i) {
+  __shared__ int chosen[4][KM];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = blockIdx.x * 4 + wave;
+  if (r >= rows) return;  // (whole waves; no workgroup barrier below)
+  const int S = (V + 15) / 16, j = r / B;
+  float mx[kSlabNS];
+  const SlabRow rs = slab_row_stats(stats + (int64_t)r * S, S, lane, mx);
+  // each lane's best KM slabs, sorted; then k wave rounds pick the row's k best slabs
+  float tv[KM];
+  int ti[KM];
+#pragma unroll
+  for (int u = 0; u < KM; ++u) tv[u] = -INFINITY, ti[u] = 0x7fffffff;
+#pragma unroll
+  for (int u = 0; u < kSlabNS; ++u) {
+    const int c = lane + 64 * u;
+    if (c < S) topk_insert<KM>(tv, ti, mx[u], c);
+  }
+  for (int sel = 0; sel < k; ++sel) {
+    float best = tv[0];
+    int bidx = ti[0], bpos = lane;
+    wave_best(best, bidx, bpos);
+    if (lane == 0) chosen[wave][sel] = bidx;  // (0x7fffffff when S < k: no such slab)
+    if (lane == bpos) {
+#pragma unroll
+      for (int u = 0; u + 1 < KM; ++u) tv[u] = tv[u + 1], ti[u] = ti[u + 1];
+      tv[KM - 1] = -INFINITY, ti[KM - 1] = 0x7fffffff;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // lane 0's LDS writes before the reads below
+  // the k * 16 candidate logits, scored exactly as the full-row kernel scores them
+  const float lse = __logf(rs.se), add = prev ? prev[r] : 0.f;
+#pragma unroll
+  for (int u = 0; u < KM; ++u) tv[u] = -INFINITY, ti[u] = 0x7fffffff;
+  const float* x = logits + (int64_t)r * V;
+  for (int e = lane; e < k * 16; e += 64) {
+    const int sl = chosen[wave][e >> 4];
+    if (sl == 0x7fffffff) continue;
+    const int c = sl * 16 + (e & 15);
+    if (c >= V) continue;
+    const float xv = x[c];
+    topk_insert<KM>(tv, ti, (logsm ? (xv - rs.M) - lse : __expf(xv - rs.M) / rs.se) + add, j * V + c);
+  }
+  for (int sel = 0; sel < k; ++sel) {
+    float best = tv[0];
+    int bidx = ti[0], bpos = lane;
+    wave_best(best, bidx, bpos);
+    if (lane == 0) cand_v[(int64_t)r * k + sel] = best, cand_i[(int64_t)r * k + sel] = bidx;
+    if (lane == bpos) {
+#pragma unroll
+      for (int u = 0; u + 1 < KM; ++u) tv[u] = tv[u + 1], ti[u] = ti[u + 1];
+      tv[KM - 1] = -INFINITY, ti[KM - 1] = 0x7fffffff;
+    }
+  }
+}
+
+void beam_step_topk_slab(const float* logits, const float2* stats, const float* prev, int k_in, int B, int V, int k,
+                         int logsm, float* cand_v, int32_t* cand_i, float* out_prob, int32_t* out_src,
+                         int32_t* out_tok, hipStream_t s) {
+  require(k >= 1 && k <= 16 && k_in >= 1 && k_in * k <= 256, "beam_step_topk_slab: k in [1, 16]");
+  require(slab_select_ok(V), "beam_step_topk_slab: V must be in [1, 16384]");
+  const int rows = k_in * B, grid = (rows + 3) / 4;
+  if (k <= 4) slab_row_topk_kernel<4><<<grid, 256, 0, s>>>(logits, stats, prev, rows, B, V, k, logsm, cand_v, cand_i);
+  else if (k == 5) slab_row_topk_kernel<5><<<grid, 256, 0, s>>>(logits, stats, prev, rows, B, V, k, logsm, cand_v, cand_i);
+  else if (k <= 8) slab_row_topk_kernel<8><<<grid, 256, 0, s>>>(logits, stats, prev, rows, B, V, k, logsm, cand_v, cand_i);
+  else slab_row_topk_kernel<16><<<grid, 256, 0, s>>>(logits, stats, prev, rows, B, V, k, logsm, cand_v, cand_i);
+  beam_merge_kernel<<<B, 64, 0, s>>>(cand_v, cand_i, k_in, B, V, k, out_prob, out_src, out_tok);
+  CAPGEN_HIP(hipGetLastError());
+}
+
 __global__ void bump_seed_kernel(uint64_t* seed) { *seed += 0x9E3779B97F4A7C15ull; }
 void bump_seed(uint64_t* seed, hipStream_t s) {
   bump_seed_kernel<<<1, 1, 0, s>>>(seed);

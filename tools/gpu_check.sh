@@ -10,7 +10,7 @@ steps=("$@")
 for st in "${steps[@]}"; do
   case "$st" in
     tests)
-      timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+      timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
         > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
       tail -2 gpurun_out/gpu_tests.log ;;
     bench)
