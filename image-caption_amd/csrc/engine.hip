@@ -641,6 +641,12 @@ struct capgen_engine {
     Planner p;
     plan_acts(p, nB, nN, nT);
     CAPGEN_HIP(hipMalloc(&ws, p.used));
+    // diagnostic (CAPGEN_POISON=<byte>): fill the fresh activation workspace with that byte, so a
+    // read of a never-written element shows up deterministically (0xff: NaN in bf16 and f32)
+    if (const char* e = std::getenv("CAPGEN_POISON")) {
+      CAPGEN_HIP(hipMemset(ws, (int)std::strtol(e, nullptr, 0), p.used));
+      hz::host_sync(nullptr);
+    }
     Planner q;
     q.base = (char*)ws;
     plan_acts(q, nB, nN, nT);
@@ -1199,6 +1205,26 @@ struct capgen_engine {
   // encoder block's FFN backward, 3: after that whole block) so capgen_debug_copy_buffer can
   // compare intermediate gradients run to run (tools/bwd_bisect.py)
   void* dbg_snap[5] = {};  // stop 4: dy / d_a / v / mean / rstd of the last encoder block's MHA LayerNorm
+  // diagnostic (CAPGEN_DEBUG_ENC_SNAP=1): the encoder chain's gradient after the Wkv_all input
+  // gradient (slot Le) and after each encoder block's backward (slot l), copied on the critical
+  // stream -- capgen_debug_copy_buffer(16 + slot) -- to find the block where two runs part
+  std::vector<void*> dbg_enc;
+  size_t dbg_enc_bytes = 0;
+  bool dbg_enc_on = [] {
+    const char* e = std::getenv("CAPGEN_DEBUG_ENC_SNAP");
+    return e && e[0] == '1';
+  }();
+  void enc_snap(int slot, const void* src, size_t bytes, hipStream_t s) {
+    if (!dbg_enc_on) return;
+    if (dbg_enc.empty() || dbg_enc_bytes < bytes) {
+      hz::host_sync(nullptr);
+      for (void* q : dbg_enc) CAPGEN_HIP(hipFree(q));
+      dbg_enc.assign(L.Le + 1, nullptr);
+      for (void*& q : dbg_enc) CAPGEN_HIP(hipMalloc(&q, bytes));
+      dbg_enc_bytes = bytes;
+    }
+    CAPGEN_HIP(hipMemcpyAsync(dbg_enc[slot], src, bytes, hipMemcpyDeviceToDevice, s));
+  }
   bool dbg_snap_on = false;
   int dbg_stop = [] {
     const char* e = std::getenv("CAPGEN_DEBUG_BWD_STOP");
@@ -1488,6 +1514,7 @@ struct capgen_engine {
     } else {
       linear_dx(a.gKV, kvld, L.Wkv_all, d, gO, d, Me, L.Ld * 2 * dd, d, 0, nullptr, nullptr, s);
     }
+    enc_snap(L.Le, gO, (size_t)Me * d * es_(), s);
     if (dbg_stop == 1) return join(s);  // diagnostic (CAPGEN_DEBUG_BWD_STOP): capgen_debug_copy_buffer
     if (L.has_mf) first_region_grad(a.mfGU, B, Lq, N, d, gO, act, s);  // enc[:, 0] of U = D + enc[:, 0]
     if (!split_kv) dw_side(a.gKV, kvld, a.X[L.Le], d, L.Wkv_all, d, Me, L.Ld * 2 * dd, d, nullptr, s);
@@ -1501,6 +1528,7 @@ struct capgen_engine {
     for (int l = L.Le - 1; l >= 0; --l) {
       const auto& w = L.enc[l];
       enc_layer_bwd(w, a.enc[l], a.genc[l], a.X[l], B, N, cfg.encode_mask ? a.valid : nullptr, l, on, gO, gR, s);
+      enc_snap(l, gO, (size_t)Me * d * es_(), s);
       if (dbg_stop >= 2 && l == L.Le - 1) return join(s);  // 3, 4: after the whole block
       if (l % bucket_blocks == 0)
         (l == 0 ? bucket(w.Wqkv, enc_end(std::min(l + bucket_blocks - 1, L.Le - 1)) - w.Wqkv, s)
@@ -2006,6 +2034,7 @@ struct capgen_engine {
   ~capgen_engine() {
     if (es) (void)hipStreamSynchronize(es);
     drop_graph();
+    for (void* q : dbg_enc) (void)hipFree(q);
     if (comm) ncclCommDestroy(comm);
     for (void* p : {(void*)params, (void*)grads, (void*)am, (void*)av, (void*)shadow, (void*)pe, (void*)step,
                     (void*)adam_scal, (void*)seed, (void*)scalars, (void*)gstripe, ws, gws, (void*)stamp_ring})
@@ -2452,7 +2481,8 @@ int capgen_debug_copy_buffer(capgen_t* h, int which, void* host_dst, int64_t byt
     void* src = which == 0 ? h->a.tmp : which == 1 ? h->a.gOut : which == 2 ? h->a.gRes : which == 3 ? h->a.gKV
               : which == 4 ? h->a.genc[Le - 1].gH : which == 5 ? h->a.genc[Le - 1].gAf
               : which == 6 ? h->a.genc[Le - 1].gA1 : which == 7 ? h->a.genc[Le - 1].gQKV
-              : which >= 8 && which < 13 ? h->dbg_snap[which - 8] : nullptr;
+              : which >= 8 && which < 13 ? h->dbg_snap[which - 8]
+              : which >= 16 && which - 16 < (int)h->dbg_enc.size() ? h->dbg_enc[which - 16] : nullptr;
     require(src != nullptr, "debug_copy_buffer: which in 0..12 (8-12 need CAPGEN_DEBUG_BWD_STOP=4)");
     hz::host_sync(nullptr);
     CAPGEN_HIP(hipMemcpy(host_dst, src, (size_t)bytes, hipMemcpyDeviceToHost));

@@ -122,9 +122,27 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs g) {
   lb.store(Bs[0], tid);
   __syncthreads();
 
+  // f32 operands: blocked accumulation -- each 256-deep K panel is summed in `acc`, then added into
+  // `tot` (a two-level sum like a CPU sgemm's K blocking: ~K/256 + 64 chained roundings per output
+  // instead of K/4; at K = 2304 the single chain was ~5x further from the float64 result than the
+  // reference's CPU arithmetic on the cancelling random-init weight gradients)
+  constexpr int KPANEL = 256 / BK;
+  f32x4 tot[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) tot[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, fq = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
+    if constexpr (sizeof(T) == 4) {
+      if (kt > 0 && kt % KPANEL == 0) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) tot[i][j] += acc[i][j], acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
     if (kt + 1 < nk) {
       la.load(A, g.lda, m0, g.M, (kt + 1) * BK, g.K, tid);
       lb.load(B, g.ldb, n0, g.N, (kt + 1) * BK, g.K, tid);
@@ -164,6 +182,14 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs g) {
     __syncthreads();
   }
 
+  if constexpr (sizeof(T) == 4) {
+    if (nk > KPANEL) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] += tot[i][j];
+    }
+  }
   // ---- epilogue ----
   const float alpha = g.alpha_ptr ? g.alpha * *g.alpha_ptr : g.alpha;
   TO* __restrict__ C = reinterpret_cast<TO*>(g.C);

@@ -490,6 +490,22 @@ static void launch_bf16_tiles(const GemmArgs& g, hipStream_t s) {
       else c.splitk = 1;  // no allocation inside a capture
     }
   }
+  // diagnostic (CAPGEN_NO_KG=1): a k-group variant runs as its one-group tile with grid split-K =
+  // KG -- the same partial sums in the same order (bit-identical by construction, gemm_tile)
+  static const bool no_kg = [] {
+    const char* e = std::getenv("CAPGEN_NO_KG");
+    return e && e[0] == '1';
+  }();
+  if (no_kg && kVariantKG[c.variant] > 1 && c.splitk == 1) {
+    static const int base[NVARIANTS + 1] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                            0, 0, 0, 0, 0, 0, 0, 6, 7, 21, 6, 17, 4, 5, 17};
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    CAPGEN_HIP(hipStreamIsCapturing(s, &st));
+    if (st == hipStreamCaptureStatusNone) {
+      c.splitk = kVariantKG[c.variant], c.variant = base[c.variant];
+      ensure_ws(s, splitk_bytes(g, c.splitk));
+    }
+  }
   launch_variant<TO, TA, TB>(c.variant, g, s, c.splitk);
 }
 

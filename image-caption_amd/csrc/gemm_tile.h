@@ -191,6 +191,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&a
 #ifdef CAPGEN_GEMM_ABLATE
 #define ABL_NO_MFMA (proto & 1024)
 #define ABL_NO_DMA (proto & 2048)
+#define ABL_DMA_FIRST (proto & 8192)  // 4-wave tiles take the DMA-issue-first k-step order too
 #define ABL_T(slot)                                                                                   \
   do {                                                                                                \
     if ((proto & 4096) && g.stamp && blockIdx.x == 0 && threadIdx.x == 0) {                           \
@@ -201,6 +202,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&a
 #else
 #define ABL_NO_MFMA 0
 #define ABL_NO_DMA 0
+#define ABL_DMA_FIRST 0
 #define ABL_T(slot) \
   do {              \
   } while (0)
@@ -280,7 +282,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int mt, int nt, int
         __builtin_amdgcn_s_barrier();  // ... for every wave; stage (s-1) % STAGES is free again
         if (kt < 8) ABL_T(3 + 4 * kt);
         const char* st = smem + s * SB;
-        if constexpr (NW * KG > 4) {
+        if (NW * KG > 4 || ABL_DMA_FIRST) {
           // 8- and 16-wave tiles (and k-group tiles): DMA issue, then per 32-deep step its fragment
           // reads + MFMAs (hipcc reuses the fragment registers across the two steps).  Measured
           // against the read-everything-first order below (tools/gemm_splitk_sweep.py, r03): that

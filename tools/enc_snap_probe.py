@@ -1,0 +1,74 @@
+"""Where two engines' bucketed c2s bf16 steps part (the intermittent encoder-side divergence):
+every engine runs forward/backward then two train_steps with CAPGEN_DEBUG_ENC_SNAP=1; after each
+train_step the encoder chain's gradient after the Wkv_all input gradient and after every encoder
+block is copied out.  Engine 0 is compared with engines 1..n-1: first differing slot per step."""
+import ctypes as C
+import json
+import os
+import sys
+
+os.environ["CAPGEN_DEBUG_ENC_SNAP"] = "1"
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "image-caption_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from capgen import _lib  # noqa: E402
+from capgen.engine import Engine  # noqa: E402
+from capgen.params import fixture_state_dict  # noqa: E402
+from golden_util import load_fixture  # noqa: E402
+
+lib = _lib.load()
+cfg, seed, z = load_fixture("c2s")
+cfg = cfg.replace(dropout=0.3, attention_dropout=0.3)
+f, p, c = [torch.from_numpy(z[k]).to("cuda:0") for k in ("feats", "pos", "caps")]
+Le = cfg.encode_num_blocks
+Me = f.shape[0] * f.shape[1]
+nel = Me * cfg.encode_input_size
+
+
+def snaps(e):
+    out = []
+    for slot in list(range(Le, -1, -1)):
+        buf = np.empty(nel, dtype=np.uint16)
+        _lib.check(lib.capgen_debug_copy_buffer(e.h, 16 + slot, buf.ctypes.data_as(C.c_void_p), nel * 2))
+        out.append(buf)
+    return out  # [eO, after block Le-1, ..., after block 0]
+
+
+def run():
+    e = Engine(cfg.replace(dtype="bf16"), "cuda:0")
+    e.load_state_dict(fixture_state_dict(cfg, seed=seed, with_buffer=False))
+    e.set_rng_seed(11)
+    e.forward(f, p, c)
+    e.backward()
+    fb = snaps(e)
+    e.set_rng_seed(11)
+    e.train_step(f, p, c)
+    s1 = snaps(e)
+    e.train_step(f, p, c)
+    s2 = snaps(e)
+    g = e.grads_state_dict()
+    del e
+    return fb, s1, s2, g
+
+
+def first_diff(a, b):
+    for i, (x, y) in enumerate(zip(a, b)):
+        if not np.array_equal(x, y):
+            xf = (x.astype(np.uint32) << 16).view(np.float32)
+            yf = (y.astype(np.uint32) << 16).view(np.float32)
+            rows = np.nonzero((x != y).reshape(Me, -1).any(1))[0]
+            return {"slot": "eO" if i == 0 else f"after block {Le - i}", "n_elems": int((x != y).sum()),
+                    "rows": rows[:12].tolist(), "n_rows": int(len(rows)),
+                    "max_abs": float(np.nanmax(np.abs(xf - yf)))}
+    return None
+
+
+runs = [run() for _ in range(int(os.environ.get("N_ENGINES", "4")))]
+for k in range(1, len(runs)):
+    rep = {"engine": k}
+    for j, name in enumerate(("fb", "step1", "step2")):
+        rep[name] = first_diff(runs[0][j], runs[k][j])
+    print(json.dumps(rep), flush=True)

@@ -1,0 +1,8 @@
+#!/bin/bash
+set -o pipefail
+mkdir -p gpurun_out
+: > gpurun_out/snap.log
+for rep in 1 2 3 4 5 6; do
+  CAPGEN_FWD_GRAPH=0 timeout -k 10 180 python -u tools/enc_snap_probe.py 2>&1 | grep '^{' >> gpurun_out/snap.log || { echo fail; exit 1; }
+done
+cat gpurun_out/snap.log
