@@ -77,6 +77,19 @@ def main():
         torch.cuda.synchronize()
         ref = torch.relu(X.float() @ W1.float().t() + b1).to(torch.bfloat16)
         row["pair_vs_torch_H_maxabs"] = float((Hr.float() - ref.float()).abs().max())
+        # one launch first, timed on the host, with the give-up count (a dependency wait that never
+        # ends is bounded in the kernel: each give-up costs ~0.1 s)
+        import time
+        gv0 = C.c_int(0)
+        _lib.check(lib.capgen_debug_persist_giveups(1, C.byref(gv0)))
+        t0 = time.perf_counter()
+        with torch.cuda.stream(s):
+            persist(512, 1)
+        torch.cuda.synchronize()
+        _lib.check(lib.capgen_debug_persist_giveups(1, C.byref(gv0)))
+        print(json.dumps({"shape": name, "first_launch_ms": round((time.perf_counter() - t0) * 1e3, 2),
+                          "giveups": gv0.value, "H_equal": bool(torch.equal(H, Hr)), "Y_equal": bool(torch.equal(Y, Yr))}),
+              flush=True)
         exact = True
         for grid in (256, 512, 768):
             for rep in range(3):
