@@ -1,5 +1,7 @@
 // capgen — GEMM launcher interface (see gemm.hip for the kernel).
 #pragma once
+#include <type_traits>
+
 #include "capgen_common.h"
 
 namespace capgen {
@@ -8,8 +10,10 @@ enum class DType : int { F32 = 0, BF16 = 1 };
 
 inline size_t dsize(DType t) { return t == DType::F32 ? 4 : 2; }
 
+// (explicit pad_ fields: no implicit padding, so a GemmArgs / GemmGroup is fully described by its
+// bytes -- the grouped launch's device-resident argument table keys on them)
 struct GemmArgs {
-  int M = 0, N = 0, K = 0;
+  int M = 0, N = 0, K = 0, pad0_ = 0;
   const void* A = nullptr;
   int64_t lda = 0;
   const void* B = nullptr;
@@ -20,6 +24,7 @@ struct GemmArgs {
   const void* aux = nullptr;        // same dtype as A/B: zero the output where aux[m][n] <= 0
   int64_t ldaux = 0;
   float alpha = 1.f;
+  int pad1_ = 0;
   const float* alpha_ptr = nullptr;  // device scalar multiplied into alpha (e.g. 1/count)
   int beta = 0;                      // 1: accumulate into C
   int prio = 0;                      // 1: critical-path launch, waves raise their issue priority
@@ -31,6 +36,7 @@ struct GemmArgs {
   int relu = 0;
   float* colsum = nullptr;           // += column sums of the (post-epilogue, beta=0) output, f32 [N]
   int colsum_stripes = 1;            // workgroup w adds into colsum + (w % stripes) * colsum_stride
+  int pad2_ = 0;
   int64_t colsum_stride = 0;
   // fused cross-entropy epilogue (bf16 NT path only; classifier + CE, model.py:93-96): per row m
   // and 16-column slab c, v = alpha * acc + bias, mx = max(v), C[m][n] = exp(v - mx) (bf16) and
@@ -47,7 +53,10 @@ struct GemmArgs {
   int64_t dec_ld = 0;
   uint64_t* stamp = nullptr;  // diagnostic timestamps (capgen_common.h StampScope); grouped: p[0]'s
   int wt = -1;                // write-through (sc1) C stores (bf16 path): 1/0, -1 = wt_default()
+  int pad3_ = 0;
 };
+// 4 ints + 28 eight-byte fields (pointers, int64s, int/float pairs): the size leaves no room for padding
+static_assert(sizeof(GemmArgs) == 16 + 28 * 8, "GemmArgs must have no padding");
 
 // Independent GEMMs of one layout launched as ONE grid (tiles problem after problem).
 constexpr int kMaxGroup = 8;
@@ -57,6 +66,7 @@ struct GemmGroup {
   int tiles_n[kMaxGroup] = {};    // column tiles of problem i
   GemmArgs p[kMaxGroup];
 };
+static_assert(sizeof(GemmGroup) == 4 * (1 + 2 * kMaxGroup + 1) + kMaxGroup * sizeof(GemmArgs), "GemmGroup must have no padding");
 
 // ta: A stored [K][M] (else [M][K]); tb: B stored [K][N] (else [N][K]).
 void gemm(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t s);

@@ -39,6 +39,7 @@
 #include <tuple>
 #include <vector>
 
+#include <cstring>
 #include "gemm.h"
 #include "hazard.h"
 #include "gemm_tile.h"
@@ -83,6 +84,25 @@ template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int STA
 __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_grouped_kernel(GemmGroup gg, int nblk, int G,
                                                                         const void* zero) {
   __shared__ __attribute__((aligned(1024))) char smem[TileCfg<TA, TB, BM, BN, WM, WN, STAGES>::SMEM];
+  StampScope stamp_scope(gg.p[0].stamp);
+  for (int b = blockIdx.x; b < nblk; b += G) {
+    if (b != (int)blockIdx.x) __syncthreads();  // the previous tile's LDS reads are done
+    const int slot = xcd_slot(b, nblk);
+    int q = 0;
+    while (q + 1 < gg.n && slot >= gg.start[q + 1]) ++q;
+    const int tile = slot - gg.start[q];
+    const int mt = tile / gg.tiles_n[q], nt = tile % gg.tiles_n[q];
+    gemm_tile<TO, TA, TB, BM, BN, WM, WN, STAGES>(gg.p[q], mt, nt, tile, 0, 1, zero, nullptr, nullptr, smem);
+  }
+}
+
+// The same, with the group description read from a device-resident table (grouped_args_dev): the
+// launch carries one pointer instead of ~1.7 KB of kernel arguments (host enqueue cost)
+template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int STAGES>
+__global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_grouped_dev_kernel(const GemmGroup* __restrict__ ggp,
+                                                                            int nblk, int G, const void* zero) {
+  __shared__ __attribute__((aligned(1024))) char smem[TileCfg<TA, TB, BM, BN, WM, WN, STAGES>::SMEM];
+  const GemmGroup& gg = *ggp;
   StampScope stamp_scope(gg.p[0].stamp);
   for (int b = blockIdx.x; b < nblk; b += G) {
     if (b != (int)blockIdx.x) __syncthreads();  // the previous tile's LDS reads are done
@@ -518,11 +538,51 @@ static void launch_bf16_layout(const GemmArgs& g, bool ta, bool tb, hipStream_t 
 }
 
 // ---- grouped launch ---------------------------------------------------------------------
+// Device-resident copies of grouped-launch descriptions, keyed by their bytes: a step issues the
+// same ~16 groups every time (same pointers), so each is copied to the device once and later
+// launches pass its address.  Entries are never freed (a captured graph may hold one); the table
+// is bounded (kGroupTableCap entries per device, then launches fall back to by-value arguments).
+// CAPGEN_GROUP_ARGS_DEV=0 restores by-value arguments.
+constexpr int kGroupTableCap = 2048;
+struct GroupTable {
+  std::map<uint64_t, std::vector<std::pair<GemmGroup, const GemmGroup*>>> by_hash;
+  GemmGroup* dev = nullptr;
+  int used = 0;
+};
+GroupTable g_group_table[64];
+std::mutex g_group_table_mu;
+
+const GemmGroup* grouped_args_dev(const GemmGroup& gg, int dev, hipStream_t s) {
+  static const bool on = [] {
+    const char* e = std::getenv("CAPGEN_GROUP_ARGS_DEV");
+    return !(e && e[0] == '0');
+  }();
+  if (!on) return nullptr;
+  const unsigned char* b = reinterpret_cast<const unsigned char*>(&gg);
+  uint64_t h = 1469598103934665603ull;
+  for (size_t i = 0; i < sizeof(GemmGroup); ++i) h = (h ^ b[i]) * 1099511628211ull;
+  std::lock_guard<std::mutex> lk(g_group_table_mu);
+  GroupTable& t = g_group_table[dev];
+  auto& bucket = t.by_hash[h];
+  for (auto& e : bucket)
+    if (std::memcmp(&e.first, &gg, sizeof(GemmGroup)) == 0) return e.second;
+  if (t.used >= kGroupTableCap) return nullptr;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  CAPGEN_HIP(hipStreamIsCapturing(s, &st));
+  if (st != hipStreamCaptureStatusNone) return nullptr;  // no synchronous copy inside a capture
+  if (!t.dev) CAPGEN_HIP(hipMalloc(&t.dev, sizeof(GemmGroup) * kGroupTableCap));
+  GemmGroup* slot = t.dev + t.used++;
+  // synchronous: complete before any later launch reads it; the slot is fresh (no reader yet)
+  CAPGEN_HIP(hipMemcpy(slot, &gg, sizeof(GemmGroup), hipMemcpyHostToDevice));
+  bucket.push_back({gg, slot});
+  return slot;
+}
+
 template <typename TO, bool TA, bool TB, int BM, int BN, int WM, int WN, int ST>
 static void launch_group_cfg(const GemmArgs* ps, int n, hipStream_t s) {
   int dev = 0;
   CAPGEN_HIP(hipGetDevice(&dev));
-  GemmGroup gg;
+  GemmGroup gg;  // (no padding bytes: gemm.h; unused problem slots stay value-initialised)
   gg.n = n;
   int tot = 0;
   for (int i = 0; i < n; ++i) {
@@ -544,7 +604,10 @@ static void launch_group_cfg(const GemmArgs* ps, int n, hipStream_t s) {
     return std::max(8, n / 8 * 8);
   }();
   const int G = cap > 0 ? std::min(tot, cap) : tot;
-  gemm_bf16_grouped_kernel<TO, TA, TB, BM, BN, WM, WN, ST><<<G, 64 * WM * WN, 0, s>>>(gg, tot, G, g_zero_page[dev]);
+  if (const GemmGroup* d = grouped_args_dev(gg, dev, s))
+    gemm_bf16_grouped_dev_kernel<TO, TA, TB, BM, BN, WM, WN, ST><<<G, 64 * WM * WN, 0, s>>>(d, tot, G, g_zero_page[dev]);
+  else
+    gemm_bf16_grouped_kernel<TO, TA, TB, BM, BN, WM, WN, ST><<<G, 64 * WM * WN, 0, s>>>(gg, tot, G, g_zero_page[dev]);
 }
 
 // the variants worth a grouped launch (many tiles already: no split-K)
