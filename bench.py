@@ -76,11 +76,11 @@ def _pmc_traffic():
     """HBM bytes per train step from the COMMITTED rocprofv3 PMC passes (FETCH_SIZE x2 per the
     gfx950 correction + WRITE_SIZE, summed over one step's kernels; tools/pmcsum.py) -- a file
     measured on this code by tools/round_profile.sh, not in this run (PMC needs its own passes)."""
-    path = os.path.join(REPO, "profiles", "r02_pmc_traffic.json")
-    if not os.path.exists(path):
-        path = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
-    if not os.path.exists(path):
+    import glob
+    found = sorted(glob.glob(os.path.join(REPO, "profiles", "r[0-9][0-9]_pmc_traffic.json")))
+    if not found:
         return None
+    path = found[-1]  # the newest round's passes
     with open(path) as fh:
         d = json.load(fh)
     return {"bytes_per_step": d["hbm_bytes_per_step"], "source": os.path.relpath(path, REPO)}

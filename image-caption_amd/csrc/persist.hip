@@ -54,9 +54,11 @@ __global__ void __launch_bounds__(256) ffn_persist_kernel(FfnTask p) {
       const int u = t - n1, mt = u / p.tn2, nt = u % p.tn2;
       if (threadIdx.x == 0) {
         int spins = 0;
-        while (__hip_atomic_load(p.done + mt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p.tn1) {
+        // the poll is an atomic read-modify-write (+0): a plain or sc1 load is served from this XCD's
+        // L2, which measured never seeing the other XCDs' adds here (every wait gave up)
+        while (__hip_atomic_fetch_add(p.done + mt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p.tn1) {
           __builtin_amdgcn_s_sleep(2);
-          if (++spins > (1 << 22)) {  // ~0.1 s: give up (results wrong, the grid still drains)
+          if (++spins > (1 << 16)) {  // bounded: give up (results wrong, the grid still drains)
             __hip_atomic_fetch_add(p.queue + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
           }

@@ -71,10 +71,12 @@ def main():
                 return round(e0.elapsed_time(e1) / (3 * args.reps) * 1e3, 2)
 
         row = {"shape": name, "M": M, "d": d, "fe": fe}
+        print(f"[{name}] inputs ready", flush=True)
         _lib.check(lib.capgen_debug_gemm_variant(V7))
         with torch.cuda.stream(s):
             pair(Hr, Yr)
         torch.cuda.synchronize()
+        print(f"[{name}] plain pair done", flush=True)
         ref = torch.relu(X.float() @ W1.float().t() + b1).to(torch.bfloat16)
         row["pair_vs_torch_H_maxabs"] = float((Hr.float() - ref.float()).abs().max())
         # one launch first, timed on the host, with the give-up count (a dependency wait that never
