@@ -2482,7 +2482,15 @@ int capgen_debug_copy_buffer(capgen_t* h, int which, void* host_dst, int64_t byt
               : which == 4 ? h->a.genc[Le - 1].gH : which == 5 ? h->a.genc[Le - 1].gAf
               : which == 6 ? h->a.genc[Le - 1].gA1 : which == 7 ? h->a.genc[Le - 1].gQKV
               : which >= 8 && which < 13 ? h->dbg_snap[which - 8]
-              : which >= 16 && which - 16 < (int)h->dbg_enc.size() ? h->dbg_enc[which - 16] : nullptr;
+              : which >= 16 && which - 16 < (int)h->dbg_enc.size() ? h->dbg_enc[which - 16]
+              // 32 + 8 l + j: encoder block l's per-block gradient buffers (never overwritten later in
+              // the backward): j = 0 gAf, 1 gH, 2 gA1, 3 gATT1, 4 gQKV
+              : which >= 32 && (which - 32) / 8 < Le && (which - 32) % 8 < 5
+                  ? (&h->a.genc[(which - 32) / 8].gAf)[(which - 32) % 8 == 0 ? 0 : (which - 32) % 8 == 1 ? 1
+                                                        : (which - 32) % 8 == 2 ? 2 : (which - 32) % 8 == 3 ? 3 : 4]
+              // 80 + l: the forward's encoder activations X[l] (l = 0 .. Le: embedding output .. encoder output)
+              : which >= 80 && which - 80 <= Le ? h->a.X[which - 80]
+                  : nullptr;
     require(src != nullptr, "debug_copy_buffer: which in 0..12 (8-12 need CAPGEN_DEBUG_BWD_STOP=4)");
     hz::host_sync(nullptr);
     CAPGEN_HIP(hipMemcpy(host_dst, src, (size_t)bytes, hipMemcpyDeviceToHost));

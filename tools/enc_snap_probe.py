@@ -28,13 +28,29 @@ Me = f.shape[0] * f.shape[1]
 nel = Me * cfg.encode_input_size
 
 
+FE = cfg.encode_hidden_size
+NAMES = []
+
+
 def snaps(e):
+    """In chain order: eO, then per block l = Le-1 .. 0: gAf, gH, gA1, gATT1, gQKV, block output."""
     out = []
-    for slot in list(range(Le, -1, -1)):
-        buf = np.empty(nel, dtype=np.uint16)
-        _lib.check(lib.capgen_debug_copy_buffer(e.h, 16 + slot, buf.ctypes.data_as(C.c_void_p), nel * 2))
+    names = []
+
+    def grab(which, n, name):
+        buf = np.empty(n, dtype=np.uint16)
+        _lib.check(lib.capgen_debug_copy_buffer(e.h, which, buf.ctypes.data_as(C.c_void_p), n * 2))
         out.append(buf)
-    return out  # [eO, after block Le-1, ..., after block 0]
+        names.append(name)
+    for l in range(Le + 1):
+        grab(80 + l, nel, f"forward X[{l}]")
+    grab(16 + Le, nel, "eO")
+    for l in range(Le - 1, -1, -1):
+        for j, (nm, n) in enumerate((("gAf", nel), ("gH", Me * FE), ("gA1", nel), ("gATT1", nel), ("gQKV", 3 * nel))):
+            grab(32 + 8 * l + j, n, f"block {l} {nm}")
+        grab(16 + l, nel, f"after block {l}")
+    NAMES[:] = names
+    return out
 
 
 def run():
@@ -60,7 +76,8 @@ def first_diff(a, b):
             xf = (x.astype(np.uint32) << 16).view(np.float32)
             yf = (y.astype(np.uint32) << 16).view(np.float32)
             rows = np.nonzero((x != y).reshape(Me, -1).any(1))[0]
-            return {"slot": "eO" if i == 0 else f"after block {Le - i}", "n_elems": int((x != y).sum()),
+            cols = np.nonzero((x != y).reshape(Me, -1).any(0))[0]
+            return {"slot": NAMES[i], "n_elems": int((x != y).sum()), "cols": cols[:12].tolist(),
                     "rows": rows[:12].tolist(), "n_rows": int(len(rows)),
                     "max_abs": float(np.nanmax(np.abs(xf - yf)))}
     return None
