@@ -27,11 +27,34 @@ def ptr(t):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--small", action="store_true", help="one 64-row block, grids 1/2/8, one launch each (hang triage)")
     args = ap.parse_args()
     lib = _lib.load()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     out = []
+    if args.small:
+        import time
+        M, d, fe = 64, 512, 2048
+        X = (torch.randn(M, d, device=dev) * 0.5).to(torch.bfloat16)
+        W1 = (torch.randn(fe, d, device=dev) / d ** 0.5).to(torch.bfloat16)
+        b1 = torch.randn(fe, device=dev) * 0.1
+        W2 = (torch.randn(d, fe, device=dev) / fe ** 0.5).to(torch.bfloat16)
+        H = torch.empty(M, fe, device=dev, dtype=torch.bfloat16)
+        Y = torch.empty(M, d, device=dev, dtype=torch.bfloat16)
+        s = torch.cuda.Stream(dev)
+        refH = torch.relu(X.float() @ W1.float().t() + b1)
+        for grid in (1, 2, 8, 64):
+            t0 = time.perf_counter()
+            _lib.check(lib.capgen_debug_ffn_persist(M, d, fe, ptr(X), ptr(W1), ptr(b1), ptr(W2), ptr(H), ptr(Y), grid, 1,
+                                                    C.c_void_p(s.cuda_stream)))
+            torch.cuda.synchronize()
+            gv = C.c_int(0)
+            _lib.check(lib.capgen_debug_persist_giveups(1, C.byref(gv)))
+            print(json.dumps({"grid": grid, "ms": round((time.perf_counter() - t0) * 1e3, 2), "giveups": gv.value,
+                              "H_maxerr": float((H.float() - refH).abs().max()),
+                              "Y_maxerr": float((Y.float() - H.float() @ W2.float().t()).abs().max())}), flush=True)
+        return
     for name, M, d, fe in (("enc FFN", 2304, 512, 2048), ("dec FFN", 1216, 512, 2048)):
         X = (torch.randn(M, d, device=dev) * 0.5).to(torch.bfloat16)
         W1 = (torch.randn(fe, d, device=dev) / d ** 0.5).to(torch.bfloat16)
