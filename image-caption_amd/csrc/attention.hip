@@ -375,9 +375,14 @@ __device__ __forceinline__ void bf16x8_to_f(const uint4& u, float (&f)[8]) {
     f[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
   }
 }
+// Group mode with kv_lds (CAPGEN_DECODE_GROUP_LDS, default on): the workgroup stages the image's K/V
+// rows of the head in LDS once (one coalesced pass over Lk x 128 B each) and every wave takes its
+// chunks from there -- without it each of the workgroup's waves loads the same rows from L1/L2
+// (4 waves x 2048 (image, head) workgroups at C4).  Same per-lane values, same sums: bit-identical.
 template <int NIT>
 __global__ void __launch_bounds__(512) attn_decode_bf16_kernel(AttnGeom g, int G, bf16* __restrict__ o,
-                                                               float* __restrict__ probs) {
+                                                               float* __restrict__ probs, int kv_lds) {
+  __shared__ uint4 kvs[2][64 * 8];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, jr = lane >> 3, c = lane & 7;
   const bool group = G > 1;
   int b0, h, bk, qfirst, qstep;
@@ -396,16 +401,34 @@ __global__ void __launch_bounds__(512) attn_decode_bf16_kernel(AttnGeom g, int G
   const int rl = (!group && g.kv_row && lane < Lk) ? g.kv_row[(int64_t)b0 * g.kv_row_ld + lane] - bk : 0;
   uint4 kr[NIT], vr[NIT];
   bool kin[NIT];
+  if (group && kv_lds) {  // (uniform: the whole workgroup takes this branch, so the barrier is safe)
+    const bf16* k0 = kb - c * 8;
+    const bf16* v0 = vb - c * 8;
+    for (int idx = threadIdx.x; idx < Lk * 8; idx += blockDim.x) {
+      const int j = idx >> 3, cc = idx & 7;
+      kvs[0][idx] = *reinterpret_cast<const uint4*>(k0 + (int64_t)j * g.k_ld + cc * 8);
+      kvs[1][idx] = *reinterpret_cast<const uint4*>(v0 + (int64_t)j * g.v_ld + cc * 8);
+    }
+    __syncthreads();
 #pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int j = jr + 8 * it;
-    kin[it] = j < Lk;
-    const int r = g.kv_row ? __shfl(rl, j < 64 ? j : 0, 64) : 0;
-    if (kin[it]) {
-      kr[it] = *reinterpret_cast<const uint4*>(kb + (int64_t)r * g.k_bs + (int64_t)j * g.k_ld);
-      vr[it] = *reinterpret_cast<const uint4*>(vb + (int64_t)r * g.v_bs + (int64_t)j * g.v_ld);
-    } else {
-      kr[it] = vr[it] = make_uint4(0, 0, 0, 0);
+    for (int it = 0; it < NIT; ++it) {
+      const int j = jr + 8 * it;
+      kin[it] = j < Lk;
+      kr[it] = kin[it] ? kvs[0][j * 8 + c] : make_uint4(0, 0, 0, 0);
+      vr[it] = kin[it] ? kvs[1][j * 8 + c] : make_uint4(0, 0, 0, 0);
+    }
+  } else {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int j = jr + 8 * it;
+      kin[it] = j < Lk;
+      const int r = g.kv_row ? __shfl(rl, j < 64 ? j : 0, 64) : 0;
+      if (kin[it]) {
+        kr[it] = *reinterpret_cast<const uint4*>(kb + (int64_t)r * g.k_bs + (int64_t)j * g.k_ld);
+        vr[it] = *reinterpret_cast<const uint4*>(vb + (int64_t)r * g.v_bs + (int64_t)j * g.v_ld);
+      } else {
+        kr[it] = vr[it] = make_uint4(0, 0, 0, 0);
+      }
     }
   }
   const float inv_t = 1.f / g.temperature;
@@ -481,16 +504,20 @@ static void launch_decode(const AttnGeom& g, T* o, float* probs, hipStream_t s) 
     if (((g.q_bs | g.k_bs | g.v_bs | g.k_ld | g.v_ld | g.o_bs) % 8) == 0) {
       const int blocks = grouped ? g.kv_bmod * g.H : (g.B * g.H + 3) / 4;
       const int Gk = grouped ? G : 1;
-      // grouped: 4 waves share the image's queries (CAPGEN_DECODE_GROUP_WAVES = 1..8; one wave per
-      // beam row, 5 waves at beam 5, measured 25.1 vs 18.8 us)
+      // grouped: 2 waves share the image's queries (CAPGEN_DECODE_GROUP_WAVES = 1..8).  C4 beam 5,
+      // two alternating rounds per setting (round 3): 1 wave 14.7-15.7 ms/batch, 2 waves 14.2-14.5,
+      // 4 waves 14.6-14.7, 8 waves 15.1-15.2 (one wave per beam row, round 2: 25.1 vs 18.8 us/launch)
       static const int gw_env = [] {
         const char* e = std::getenv("CAPGEN_DECODE_GROUP_WAVES");
-        return e ? std::max(1, std::min(8, std::atoi(e))) : 4;
+        return e ? std::max(1, std::min(8, std::atoi(e))) : 2;
       }();
       const int nt = grouped ? 64 * gw_env : 256;
-      if (g.Lk <= 24) attn_decode_bf16_kernel<3><<<blocks, nt, 0, s>>>(g, Gk, o, probs);
-      else if (g.Lk <= 40) attn_decode_bf16_kernel<5><<<blocks, nt, 0, s>>>(g, Gk, o, probs);
-      else attn_decode_bf16_kernel<8><<<blocks, nt, 0, s>>>(g, Gk, o, probs);
+      const char* kv_env = std::getenv("CAPGEN_DECODE_GROUP_LDS");  // (read per launch: tests toggle it)
+      const int kv_lds = kv_env && kv_env[0] == '0' ? 0 : 1;
+      const int lds = grouped ? kv_lds : 0;
+      if (g.Lk <= 24) attn_decode_bf16_kernel<3><<<blocks, nt, 0, s>>>(g, Gk, o, probs, lds);
+      else if (g.Lk <= 40) attn_decode_bf16_kernel<5><<<blocks, nt, 0, s>>>(g, Gk, o, probs, lds);
+      else attn_decode_bf16_kernel<8><<<blocks, nt, 0, s>>>(g, Gk, o, probs, lds);
       CAPGEN_HIP(hipGetLastError());
       return;
     }

@@ -1398,3 +1398,18 @@ def test_slab_decode_selection_equals_full_row(monkeypatch):
                 return pr.gather(-1, ids[:, 1:T].long()[..., None]).squeeze(-1).sum(-1)
 
             assert (score(bs[diff]) - score(bf[diff])).abs().max().item() < 1e-5
+
+
+def test_grouped_decode_attention_lds_staging_bit_identical(monkeypatch):
+    """bf16 beam decode at C4 (B=256, beam 5): the grouped cross-attention with the image's K/V
+    staged in LDS once per (image, head) workgroup (CAPGEN_DECODE_GROUP_LDS, default) gives the same
+    beam ids as the per-wave register loads (same per-lane values, same sums)."""
+    _, cfg, sd, e, f, p, c = _c2_setup(B=256, dtype="bf16", weights="fixture")
+    e.set_training(False)
+    fd, pd = f.to(DEV).bfloat16(), p.to(DEV)
+    monkeypatch.setenv("CAPGEN_DECODE_GROUP_LDS", "1")
+    a = e.beam(fd, pd, 5).clone()
+    monkeypatch.setenv("CAPGEN_DECODE_GROUP_LDS", "0")
+    b = e.beam(fd, pd, 5).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
