@@ -1219,7 +1219,7 @@ struct capgen_engine {
     if (dbg_enc.empty() || dbg_enc_bytes < bytes) {
       hz::host_sync(nullptr);
       for (void* q : dbg_enc) CAPGEN_HIP(hipFree(q));
-      dbg_enc.assign(L.Le + 1, nullptr);
+      dbg_enc.assign(2 * L.Le + 1, nullptr);  // + slot Le + 1 + l: block l's gR after the dX W1 accumulate
       for (void*& q : dbg_enc) CAPGEN_HIP(hipMalloc(&q, bytes));
       dbg_enc_bytes = bytes;
     }
@@ -1300,6 +1300,7 @@ struct capgen_engine {
     const LnBwd lmha = lnb_desc(Me, d, gR, A.v1, A.m1, A.r1, w.ln1g, w.ln1b, -1, RowMask{},
                                 mk_drop(p, site(0, layer, 1), on), gO, gb.gA1);
     ffn_bwd(Me, d, L.fe, lffn, A.Y, A.H, w.W1, w.b1, w.W2, gb.gH, s);  // gR = grad wrt Y
+    if (layer >= 0 && layer < L.Le) enc_snap(L.Le + 1 + layer, gR, (size_t)Me * d * es_(), s);
     if (dbg_stop == 2 && layer == L.Le - 1) return;
     dbg_snap_on = layer == L.Le - 1;
     if (dbg_stop == 4 && dbg_snap_on && !dbg_snap[0])

@@ -7,7 +7,9 @@ import json
 import os
 import sys
 
-os.environ["CAPGEN_DEBUG_ENC_SNAP"] = "1"
+SNAP = os.environ.get("SNAP", "0") == "1"  # 1: also copy the chain gradient during the run (perturbs timing)
+if SNAP:
+    os.environ["CAPGEN_DEBUG_ENC_SNAP"] = "1"
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "image-caption_amd"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -33,7 +35,7 @@ NAMES = []
 
 
 def snaps(e):
-    """In chain order: eO, then per block l = Le-1 .. 0: gAf, gH, gA1, gATT1, gQKV, block output."""
+    """In chain order: eO, then per block l = Le-1 .. 0: gAf, gH, (gR), gA1, gATT1, gQKV, block output."""
     out = []
     names = []
 
@@ -44,11 +46,15 @@ def snaps(e):
         names.append(name)
     for l in range(Le + 1):
         grab(80 + l, nel, f"forward X[{l}]")
-    grab(16 + Le, nel, "eO")
+    if SNAP:
+        grab(16 + Le, nel, "eO")
     for l in range(Le - 1, -1, -1):
         for j, (nm, n) in enumerate((("gAf", nel), ("gH", Me * FE), ("gA1", nel), ("gATT1", nel), ("gQKV", 3 * nel))):
             grab(32 + 8 * l + j, n, f"block {l} {nm}")
-        grab(16 + l, nel, f"after block {l}")
+            if SNAP and nm == "gH":
+                grab(16 + Le + 1 + l, nel, f"block {l} gR")
+        if SNAP:
+            grab(16 + l, nel, f"after block {l}")
     NAMES[:] = names
     return out
 
@@ -61,7 +67,11 @@ def run():
     e.backward()
     fb = snaps(e)
     e.set_rng_seed(11)
-    e.train_step(f, p, c)
+    if os.environ.get("ALT") == "1":  # a different batch for step 1 (the two images swapped): a read of a
+        # line left from the previous call would now differ grossly, not by an ulp
+        e.train_step(f.flip(0).contiguous(), p.flip(0).contiguous(), c.flip(0).contiguous())
+    else:
+        e.train_step(f, p, c)
     s1 = snaps(e)
     e.train_step(f, p, c)
     s2 = snaps(e)
