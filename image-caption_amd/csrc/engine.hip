@@ -1225,6 +1225,14 @@ struct capgen_engine {
     }
     CAPGEN_HIP(hipMemcpyAsync(dbg_enc[slot], src, bytes, hipMemcpyDeviceToDevice, s));
   }
+  // diagnostic (CAPGEN_DEBUG_ENC_CHAIN=1): every encoder block's gR (slot l) and block-input
+  // gradient (slot Le + l) in buffers of their own, readable after the call without in-run copies
+  std::vector<void*> dbg_chain;
+  void* dbg_eO = nullptr;  // the encoder chain's starting gradient (which = 13)
+  bool dbg_chain_on = [] {
+    const char* e = std::getenv("CAPGEN_DEBUG_ENC_CHAIN");
+    return e && e[0] == '1';
+  }();
   bool dbg_snap_on = false;
   int dbg_stop = [] {
     const char* e = std::getenv("CAPGEN_DEBUG_BWD_STOP");
@@ -1290,15 +1298,19 @@ struct capgen_engine {
 
   // backward of enc_layer_fwd: gO = grad wrt Xout on entry, grad wrt X on exit; gR scratch
   void enc_layer_bwd(const EncLayerOff& w, EncAct& A, Acts::GradBufs& gb, const void* X, int B, int N,
-                     const uint8_t* valid, int layer, bool on, void* gO, void* gR, hipStream_t s) {
+                     const uint8_t* valid, int layer, bool on, void* gO, void* gR, hipStream_t s,
+                     void* gO_out = nullptr) {
+    // gO_out (diagnostic, CAPGEN_DEBUG_ENC_CHAIN): the block-input gradient goes to its own buffer
+    // instead of overwriting gO in place
     const int Me = B * N, d = L.d, He = L.He, dke = d / He;
+    void* go = gO_out ? gO_out : gO;
     const float p = cfg.dropout, pa = cfg.attention_dropout;
     RowMask mask{};
     mask.valid = valid;
     const LnBwd lffn = lnb_desc(Me, d, gO, A.v2, A.m2, A.r2, w.ln2g, w.ln2b, w.b2, mask, mk_drop(p, site(0, layer, 2), on),
                                 gR, gb.gAf);
     const LnBwd lmha = lnb_desc(Me, d, gR, A.v1, A.m1, A.r1, w.ln1g, w.ln1b, -1, RowMask{},
-                                mk_drop(p, site(0, layer, 1), on), gO, gb.gA1);
+                                mk_drop(p, site(0, layer, 1), on), go, gb.gA1);
     ffn_bwd(Me, d, L.fe, lffn, A.Y, A.H, w.W1, w.b1, w.W2, gb.gH, s);  // gR = grad wrt Y
     if (layer >= 0 && layer < L.Le) enc_snap(L.Le + 1 + layer, gR, (size_t)Me * d * es_(), s);
     if (dbg_stop == 2 && layer == L.Le - 1) return;
@@ -1318,7 +1330,7 @@ struct capgen_engine {
     dbg_snap_on = false;
     attb(g, A.P, gb.gATT1, gb.gQKV, at(gb.gQKV, d), at(gb.gQKV, 2 * d), act, s);
     dw_side(gb.gQKV, 3 * d, X, d, w.Wqkv, d, Me, 3 * d, d, nullptr, s);
-    linear_dx(gb.gQKV, 3 * d, w.Wqkv, d, gO, d, Me, 3 * d, d, 1, nullptr, nullptr, s);  // gO = grad wrt X
+    linear_dx(gb.gQKV, 3 * d, w.Wqkv, d, go, d, Me, 3 * d, d, 1, nullptr, nullptr, s);  // gO = grad wrt X
   }
 
   // backward of image_objects_fwd: gX0 = grad wrt a.X[0] -> embedding weight gradient
@@ -1505,6 +1517,7 @@ struct capgen_engine {
     // the encoder chain must not overwrite gO (read by the decoder-embedding branch on es2):
     // it runs on the other residual buffer and on tmp (free during backward)
     gO = eO;
+    dbg_eO = eO;
     gR = a.tmp;
     if (split_kv) {  // block 0's term + the f32 sum of blocks Ld-1 .. 1 (summed on es2)
       hz::wait(s, ev_part);
@@ -1526,9 +1539,19 @@ struct capgen_engine {
     bucket(L.Wel, L.dec[0].Wqkv - L.Wel, s, false);       // word-embedding projection
     bucket(L.emb, L.enc_lng - L.emb, s, false);           // word embedding table
     bucket(L.dec_lng, L.total - L.dec_lng, s, false);     // decoder LN / biases, classifier bias
+    if (dbg_chain_on && dbg_chain.empty()) {
+      hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+      CAPGEN_HIP(hipStreamIsCapturing(s, &st));
+      require(st == hipStreamCaptureStatusNone, "CAPGEN_DEBUG_ENC_CHAIN: first backward must be eager");
+      dbg_chain.assign(2 * L.Le, nullptr);
+      for (void*& q : dbg_chain) CAPGEN_HIP(hipMalloc(&q, (size_t)Me * d * es_()));
+    }
     for (int l = L.Le - 1; l >= 0; --l) {
       const auto& w = L.enc[l];
-      enc_layer_bwd(w, a.enc[l], a.genc[l], a.X[l], B, N, cfg.encode_mask ? a.valid : nullptr, l, on, gO, gR, s);
+      void* const gRl = dbg_chain_on ? dbg_chain[l] : gR;
+      void* const gOl = dbg_chain_on ? dbg_chain[L.Le + l] : nullptr;
+      enc_layer_bwd(w, a.enc[l], a.genc[l], a.X[l], B, N, cfg.encode_mask ? a.valid : nullptr, l, on, gO, gRl, s, gOl);
+      if (gOl) gO = gOl;
       enc_snap(l, gO, (size_t)Me * d * es_(), s);
       if (dbg_stop >= 2 && l == L.Le - 1) return join(s);  // 3, 4: after the whole block
       if (l % bucket_blocks == 0)
@@ -2036,6 +2059,7 @@ struct capgen_engine {
     if (es) (void)hipStreamSynchronize(es);
     drop_graph();
     for (void* q : dbg_enc) (void)hipFree(q);
+    for (void* q : dbg_chain) (void)hipFree(q);
     if (comm) ncclCommDestroy(comm);
     for (void* p : {(void*)params, (void*)grads, (void*)am, (void*)av, (void*)shadow, (void*)pe, (void*)step,
                     (void*)adam_scal, (void*)seed, (void*)scalars, (void*)gstripe, ws, gws, (void*)stamp_ring})
@@ -2483,6 +2507,7 @@ int capgen_debug_copy_buffer(capgen_t* h, int which, void* host_dst, int64_t byt
               : which == 4 ? h->a.genc[Le - 1].gH : which == 5 ? h->a.genc[Le - 1].gAf
               : which == 6 ? h->a.genc[Le - 1].gA1 : which == 7 ? h->a.genc[Le - 1].gQKV
               : which >= 8 && which < 13 ? h->dbg_snap[which - 8]
+              : which == 13 ? h->dbg_eO
               : which >= 16 && which - 16 < (int)h->dbg_enc.size() ? h->dbg_enc[which - 16]
               // 32 + 8 l + j: encoder block l's per-block gradient buffers (never overwritten later in
               // the backward): j = 0 gAf, 1 gH, 2 gA1, 3 gATT1, 4 gQKV
@@ -2491,6 +2516,20 @@ int capgen_debug_copy_buffer(capgen_t* h, int which, void* host_dst, int64_t byt
                                                         : (which - 32) % 8 == 2 ? 2 : (which - 32) % 8 == 3 ? 3 : 4]
               // 80 + l: the forward's encoder activations X[l] (l = 0 .. Le: embedding output .. encoder output)
               : which >= 80 && which - 80 <= Le ? h->a.X[which - 80]
+              // 128 + 8 l + j: encoder block l's saved forward tensors: j = 0 att, 1 v1, 2 m1, 3 r1, 4 Y,
+              // 5 v2, 6 m2, 7 r2
+              : which >= 128 && (which - 128) / 8 < Le
+                  ? ((which - 128) % 8 == 0 ? h->a.enc[(which - 128) / 8].att
+                     : (which - 128) % 8 == 1 ? h->a.enc[(which - 128) / 8].v1
+                     : (which - 128) % 8 == 2 ? (void*)h->a.enc[(which - 128) / 8].m1
+                     : (which - 128) % 8 == 3 ? (void*)h->a.enc[(which - 128) / 8].r1
+                     : (which - 128) % 8 == 4 ? h->a.enc[(which - 128) / 8].Y
+                     : (which - 128) % 8 == 5 ? h->a.enc[(which - 128) / 8].v2
+                     : (which - 128) % 8 == 6 ? (void*)h->a.enc[(which - 128) / 8].m2
+                                             : (void*)h->a.enc[(which - 128) / 8].r2)
+              // 96 + l: block l's gR, 112 + l: block l's input gradient (CAPGEN_DEBUG_ENC_CHAIN=1)
+              : which >= 96 && which < 96 + Le && !h->dbg_chain.empty() ? h->dbg_chain[which - 96]
+              : which >= 112 && which < 112 + Le && !h->dbg_chain.empty() ? h->dbg_chain[Le + which - 112]
                   : nullptr;
     require(src != nullptr, "debug_copy_buffer: which in 0..12 (8-12 need CAPGEN_DEBUG_BWD_STOP=4)");
     hz::host_sync(nullptr);

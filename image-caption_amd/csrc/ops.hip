@@ -124,9 +124,31 @@ __global__ void __launch_bounds__(NT) ln_bwd_kernel(LnBwd a) {
       on[u] = m < a.M;
       if (on[u]) {
         const int64_t base = (int64_t)m * d + c0;
-        load_f<T, DPL>(reinterpret_cast<const T*>(a.dy) + base, dy[u]);
-        load_f<T, DPL>(reinterpret_cast<const T*>(a.v) + base, v[u]);
-        mean[u] = a.mean[m], rstd[u] = a.rstd[m];
+        if constexpr (sizeof(T) == 2 && DPL % 2 == 0) {
+          if (a.coh & 2) {  // diagnostic: system-scope (sc0 sc1) loads of the row inputs
+            const uint32_t* py = reinterpret_cast<const uint32_t*>(reinterpret_cast<const T*>(a.dy) + base);
+            const uint32_t* pv = reinterpret_cast<const uint32_t*>(reinterpret_cast<const T*>(a.v) + base);
+#pragma unroll
+            for (int e = 0; e < DPL / 2; ++e) {
+              const uint32_t wy = __hip_atomic_load(py + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              const uint32_t wv = __hip_atomic_load(pv + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              dy[u][2 * e] = __uint_as_float(wy << 16), dy[u][2 * e + 1] = __uint_as_float(wy & 0xffff0000u);
+              v[u][2 * e] = __uint_as_float(wv << 16), v[u][2 * e + 1] = __uint_as_float(wv & 0xffff0000u);
+            }
+          } else {
+            load_f<T, DPL>(reinterpret_cast<const T*>(a.dy) + base, dy[u]);
+            load_f<T, DPL>(reinterpret_cast<const T*>(a.v) + base, v[u]);
+          }
+        } else {
+          load_f<T, DPL>(reinterpret_cast<const T*>(a.dy) + base, dy[u]);
+          load_f<T, DPL>(reinterpret_cast<const T*>(a.v) + base, v[u]);
+        }
+        if (a.coh & 1) {  // diagnostic: system-scope (sc0 sc1) loads of the row statistics
+          mean[u] = __hip_atomic_load(a.mean + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          rstd[u] = __hip_atomic_load(a.rstd + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        } else {
+          mean[u] = a.mean[m], rstd[u] = a.rstd[m];
+        }
         kept[u] = row_kept(a.mask, m);
       }
     }
@@ -342,6 +364,13 @@ void layernorm_bwd(const LnBwd& a_in, DType t, hipStream_t s) {
   if (a_in.M <= 0 || (skip_mask() & 4)) return;
   LnBwd a = a_in;
   if (a.wt < 0) a.wt = wt_default();
+  if (a.coh < 0) {
+    static const int coh = [] {
+      const char* e = std::getenv("CAPGEN_LNB_COH");
+      return e ? std::atoi(e) : 0;
+    }();
+    a.coh = coh;
+  }
   if (hz::active()) {
     using namespace hz;
     const int64_t row = a.d * (int64_t)dsize(t), sb = a.d * 4, ss = std::max<int64_t>(a.stripe_stride * 4, sb);

@@ -10,6 +10,9 @@ import sys
 SNAP = os.environ.get("SNAP", "0") == "1"  # 1: also copy the chain gradient during the run (perturbs timing)
 if SNAP:
     os.environ["CAPGEN_DEBUG_ENC_SNAP"] = "1"
+CHAIN = os.environ.get("CHAIN", "0") == "1"  # 1: every block's gR / input gradient in its own buffer
+if CHAIN:
+    os.environ["CAPGEN_DEBUG_ENC_CHAIN"] = "1"
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "image-caption_amd"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -46,13 +49,23 @@ def snaps(e):
         names.append(name)
     for l in range(Le + 1):
         grab(80 + l, nel, f"forward X[{l}]")
+    if CHAIN:  # the saved forward tensors the backward reads (f32 statistics as 2 x u16 per row)
+        for l in range(Le):
+            for j, nm in enumerate(("att", "v1", "m1", "r1", "Y", "v2", "m2", "r2")):
+                grab(128 + 8 * l + j, 2 * Me if nm[0] in "mr" else nel, f"forward block {l} {nm}")
     if SNAP:
         grab(16 + Le, nel, "eO")
+    if CHAIN:
+        grab(13, nel, "eO")
     for l in range(Le - 1, -1, -1):
         for j, (nm, n) in enumerate((("gAf", nel), ("gH", Me * FE), ("gA1", nel), ("gATT1", nel), ("gQKV", 3 * nel))):
             grab(32 + 8 * l + j, n, f"block {l} {nm}")
             if SNAP and nm == "gH":
                 grab(16 + Le + 1 + l, nel, f"block {l} gR")
+            if CHAIN and nm == "gH":
+                grab(96 + l, nel, f"block {l} gR")
+        if CHAIN:
+            grab(112 + l, nel, f"block {l} input grad")
         if SNAP:
             grab(16 + l, nel, f"after block {l}")
     NAMES[:] = names
@@ -87,9 +100,14 @@ def first_diff(a, b):
             yf = (y.astype(np.uint32) << 16).view(np.float32)
             rows = np.nonzero((x != y).reshape(Me, -1).any(1))[0]
             cols = np.nonzero((x != y).reshape(Me, -1).any(0))[0]
-            return {"slot": NAMES[i], "n_elems": int((x != y).sum()), "cols": cols[:12].tolist(),
+            later = [f"{NAMES[j]}:{int((u != v).sum())}" for j, (u, v) in enumerate(zip(a, b))
+                     if j > i and not np.array_equal(u, v)][:6]
+            return {"slot": NAMES[i], "n_elems": int((x != y).sum()), "cols": cols[:12].tolist(), "later": later,
                     "rows": rows[:12].tolist(), "n_rows": int(len(rows)),
-                    "max_abs": float(np.nanmax(np.abs(xf - yf)))}
+                    "max_abs": float(np.nanmax(np.abs(xf - yf))),
+                    "row_absmax": float(np.nanmax(np.abs(xf.reshape(Me, -1)[rows]))),
+                    "zero_flips": int(((xf == 0) != (yf == 0)).sum()),
+                    "ulps": int(np.abs(x.astype(np.int32) - y.astype(np.int32)).max())}
     return None
 
 
