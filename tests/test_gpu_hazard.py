@@ -101,9 +101,6 @@ def test_checker_reports_a_dropped_edge(monkeypatch):
     assert "stream" in report
 
 
-@pytest.mark.xfail(strict=False, reason="open: intermittent encoder-side last-bit divergence between two engines "
-                   "with >= 2 streams (DESIGN.md section 6, 'Open: an intermittent encoder-side divergence'); "
-                   "0 unordered pairs in the hazard log, 0 of 21 with one stream")
 def test_side_stream_delay_leaves_bf16_results_bit_identical():
     """Deterministic delay injection: a 40 us spin in front of every launch off the critical
     stream (weight-gradient groups, bias sums, decoder-embedding branch, bucket Adam).  Linear
