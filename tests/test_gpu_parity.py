@@ -480,11 +480,9 @@ def test_bf16_train_mode_matches_fp32_with_dropout():
 
 def test_grouped_weight_gradients_match_single_launches_bf16(monkeypatch):
     """bf16 weight gradients of one block computed by ONE grouped launch (default) equal the
-    per-weight launches (CAPGEN_GROUP_DW=0) up to f32 summation order (split-K choices).
-    One stream per engine (CAPGEN_STREAMS=1): the comparison is of the launch forms; the open
-    >= 2-stream last-bit divergence between engines is tracked by
-    test_bf16_weight_gradients_bit_reproducible_multistream."""
-    monkeypatch.setenv("CAPGEN_STREAMS", "1")
+    per-weight launches (CAPGEN_GROUP_DW=0) up to f32 summation order (split-K choices), with the
+    default streams (round 3 ran it on one stream while the >= 2-stream divergence was open;
+    DESIGN.md section 6)."""
     cfg, seed, z = load_fixture("c2s")
     f, p, c = _inputs(z)
     monkeypatch.setenv("CAPGEN_GROUP_DW", "0")
@@ -519,12 +517,7 @@ def test_train_step_equals_forward_backward_adam_bf16(graph, monkeypatch):
     """bf16 train_step (forward graph, grouped weight gradients, per-bucket Adam) must equal
     forward -> backward -> adam_step (one Adam pass over the whole arena): after one step every
     Linear weight bit-identical (same gradients, same Adam arithmetic); LayerNorm/bias/embedding
-    parameters up to f32-atomic summation order.  Eager steps run on one stream per engine (the
-    bucketed update is the subject; the open >= 2-stream divergence is tracked separately, DESIGN.md
-    section 6); the whole-step graph keeps the default streams (with CAPGEN_STREAMS=1 it does not
-    match the unfused update -- an untriaged issue of that diagnostic combination)."""
-    if not graph:
-        monkeypatch.setenv("CAPGEN_STREAMS", "1")
+    parameters up to f32-atomic summation order.  Default streams, eager and whole-step graph."""
     cfg, seed, z = load_fixture("c2s")
     f, p, c = _inputs(z)
     a = _engine(cfg, seed, dtype="bf16")
