@@ -48,7 +48,8 @@ struct LnBwd {
   void* y_save = nullptr;  // optional: the masked output gradient dy * rowmask (T), for layernorm_param_sums
   uint64_t* stamp = nullptr;  // diagnostic timestamps (StampScope)
   int wt = -1;                // write-through (sc1) d_res / d_a stores: 1/0, -1 = wt_default()
-  int coh = -1;  // diagnostic (CAPGEN_LNB_COH): bit 0 system-scope loads of mean / rstd, bit 1 of dy / v
+  int coh = -1;  // diagnostic (CAPGEN_LNB_COH): bit 0 system-scope loads of mean / rstd, bit 1 of dy / v,
+                // bit 2 one full wait after the row loads
 };
 void layernorm_bwd(const LnBwd& a, DType t, hipStream_t s);
 // The LayerNorm parameter sums alone -- dgamma += sum y * xhat, dbeta += sum y, dbias += sum d_a --

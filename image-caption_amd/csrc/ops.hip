@@ -152,6 +152,7 @@ __global__ void __launch_bounds__(NT) ln_bwd_kernel(LnBwd a) {
         kept[u] = row_kept(a.mask, m);
       }
     }
+    if (a.coh & 4) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // diagnostic: no partial waits
 #pragma unroll
     for (int u = 0; u < R; ++u) {
       if (!on[u]) continue;
