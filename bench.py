@@ -7,7 +7,8 @@ one 64-image batch per GPU.  N>1: launched by torch.distributed.run, one rank pe
 weak scaling (64 images per rank), exact global-mean CE.
 
 Prints ONE JSON line (rank 0).  `roofline` is the whole train step on the MFMA roof
-(519.9157 GFLOP per 64-image step, SURVEY §8(d)), plus the dominant GEMM timed alone;
+(519.9157 GFLOP per 64-image step), plus the step's dominant kernel class timed in
+the step (in-kernel timestamps);
 `cpu_baseline` times the CPU oracle (fp32 eager torch, train mode) on this host.
 """
 import argparse
@@ -40,36 +41,45 @@ def step_flops_per_image(cfg, N, T):
     return 3 * fwd - emb
 
 
-def dominant_gemm(eng, steps=50):
-    """Time the encoder FFN-up GEMM ([2304,512] x [512,2048]^T, bf16, the largest GEMM
-    class of the step) with HIP events on the launching stream."""
-    import ctypes as C
-    from capgen import _lib
-    lib = _lib.load()
-    M, Nn, K = B * N, 2048, 512
-    A = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
-    W = torch.randn(Nn, K, device="cuda", dtype=torch.bfloat16)
-    Cc = torch.empty(M, Nn, device="cuda", dtype=torch.bfloat16)
-    bias = torch.zeros(Nn, device="cuda")
-    s = torch.cuda.current_stream()
-
-    def launch():
-        _lib.check(lib.capgen_debug_gemm(M, Nn, K, C.c_void_p(A.data_ptr()), K, 0, C.c_void_p(W.data_ptr()), K, 0,
-                                         C.c_void_p(Cc.data_ptr()), Nn, 1, 1, C.c_void_p(bias.data_ptr()), 1.0, 0, 1,
-                                         C.c_void_p(s.cuda_stream)))
-    for _ in range(10):
-        launch()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(s)
+def dominant_class(eng, args, steps=3):
+    """The step's dominant kernel class measured IN the step: every GEMM / LayerNorm / attention launch
+    of a train step records the GPU's 100 MHz real-time counter at its first workgroup's start and its
+    last workgroup's end (capgen_debug_stamps, no profiler); run `steps` stamped steps after the timed
+    region, group the launches by class, and price the class with the largest summed time per step
+    (the NN input-gradient GEMMs at C2) at its algorithmic FLOPs / its average launch duration."""
+    from collections import defaultdict
+    eng.stamps(1)
+    for _ in range(2):
+        eng.train_step_raw(*args)
+    torch.cuda.synchronize()
+    cls = defaultdict(lambda: [0, 0.0, 0.0])  # launches, us, flops
     for _ in range(steps):
-        launch()
-    e1.record(s)
-    e1.synchronize()
-    ms = e0.elapsed_time(e1) / steps
-    flops = 2.0 * M * Nn * K
-    return {"kernel": "gemm_bf16_kernel (NT) enc FFN-up 2304x2048x512 (+bias,relu), autotuned variant",
-            "avg_us": round(ms * 1e3, 2), "achieved": round(flops / (ms * 1e-3) / 1e12, 1), "unit": "TFLOP/s",
-            "frac": round(flops / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4)}
+        eng.stamps(3)
+        eng.train_step_raw(*args)
+        torch.cuda.synchronize()
+        for name, t0, t1 in eng.stamps(2):
+            if t1 <= 0 or t0 <= 0 or t1 < t0:
+                continue
+            words = name.split()  # "<stream> gemm dX MxNxK" / "<stream> ln_bwd M" / ...
+            kind = " ".join(words[1:3]) if words[1] == "gemm" else words[1]
+            fl = 0.0
+            if words[1] == "gemm" and "x" in words[-1]:
+                m, n_, k = (int(x) for x in words[-1].split("x"))
+                fl = 2.0 * m * n_ * k
+            c = cls[kind]
+            c[0] += 1
+            c[1] += t1 - t0
+            c[2] += fl
+    eng.stamps(0)
+    kind, (n, us, fl) = max(cls.items(), key=lambda kv: kv[1][1])
+    avg_us = us / n
+    tf = fl / (us * 1e-6) / 1e12 if fl else None
+    names = {"gemm dX": "gemm_bf16_kernel NN input-gradient GEMMs (dX = dY . W)", "gemm fwd": "gemm_bf16_kernel NT forward GEMMs"}
+    return {"kernel": names.get(kind, kind) + ", in-step class (stamped launches: first workgroup start -> last workgroup end)",
+            "launches_per_step": round(n / steps, 1), "us_per_step": round(us / steps, 1), "avg_us": round(avg_us, 2),
+            "achieved": round(tf, 1) if tf else None, "unit": "TFLOP/s",
+            "frac": round(tf / PEAK_BF16_TFLOPS, 4) if tf else None,
+            "classes_us_per_step": {k: round(v[1] / steps, 1) for k, v in sorted(cls.items(), key=lambda kv: -kv[1][1])}}
 
 
 def _pmc_traffic():
@@ -246,7 +256,7 @@ def main():
         "host_issue_ms_per_step": round(issue_s / args.steps * 1e3, 4),
     }
     if rank == 0 and world == 1:
-        out["dominant_kernel"] = dominant_gemm(eng)
+        out["dominant_kernel"] = dominant_class(eng, (f, ft, p, c, B, N, T, loss))
         if not args.no_host_batches:
             out["host_batches"] = host_batches(eng, cfg, dev)
         if not args.no_cpu_baseline:

@@ -68,7 +68,6 @@ struct DecAct {
   float *Ps, *ms, *rs, *Pc, *mc, *rc, *mf, *rf;
 };
 
-constexpr int kLnSideSlots = 40;  // LayerNorm backward calls per backward pass with side-stream sums
 
 struct Acts {
   int B = 0, N = 0, T = 0;  // capacity
@@ -94,7 +93,6 @@ struct Acts {
   float* ce_tl;      // its target logits
   float *loss_row, *grad_scale, *loss, *loss_ce;
   void* gEnc;     // encoder-chain residual gradient while decoder block 0 finishes on es2 (overlap_dec0)
-  float* gEnc32;  // f32 partial sum of the encoder-output gradient over decoder blocks Ld-1 .. 1
   // SCST (rl.hip): per-row sample / lse / logp[sample] / entropy, per-image entropy, scalars
   int32_t* rl_sample;
   float *rl_lse, *rl_logp, *rl_ent, *rl_ent_img, *rl_score, *rl_scal;
@@ -103,8 +101,6 @@ struct Acts {
   // run later on the side stream without a write-after-read hazard.
   void *tmp, *gOut, *gRes, *gKV, *gE, *gAe, *gAd;
   void* tmpf;  // the decoder front's GEMM -> LayerNorm scratch (runs on es2 beside the encoder)
-  std::vector<void*> lns;  // per block LayerNorm: the masked output gradient for the side-stream parameter sums
-  int64_t lns_cap = 0;     // elements per lns slot
   struct GradBufs {
     void *gAf, *gH, *gA1, *gATT1, *gQKV, *gA2, *gATT2, *gQc;
   };
@@ -179,9 +175,7 @@ struct capgen_engine {
   hipStream_t ec = nullptr;   // bucket stream: per-bucket gradient all-reduce (RCCL) + Adam
   hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_b1 = nullptr, ev_b2 = nullptr, ev_cj = nullptr;
-  hipEvent_t ev_part = nullptr;  // es2: the encoder-output gradient partials are summed
   hipEvent_t ev_ff = nullptr, ev_fj = nullptr;  // forward: decoder front forked to / joined from es2
-  hipEvent_t ev_kv = nullptr;  // forward (kv_split): decoder blocks 1.. cross K/V done on es2
   float *params = nullptr, *grads = nullptr, *am = nullptr, *av = nullptr;
   bf16* shadow = nullptr;
   float* pe = nullptr;  // [max_length-1, dd] f32 sinusoid table
@@ -382,30 +376,6 @@ struct capgen_engine {
     if (stamp_on) l.stamp = stamp(s, "ln_bwd " + std::to_string(l.M));
     layernorm_bwd(l, act, s);
   }
-  // CAPGEN_LN_SUMS_SIDE=1 (experiment, off): a transformer block's LayerNorm backward on the
-  // critical stream without its parameter sums -- the kernel saves y = dy * rowmask and the
-  // dgamma / dbeta / producing-bias sums (a per-workgroup LDS reduction + striped atomics) run on
-  // es2, queued with the block's weight gradients.  Kernel level: encoder LN backward 9.98 -> 8.21
-  // us, decoder 7.93 -> 8.08 (the extra store eats the saving); step level slower (3.035 vs 3.019
-  // ms/step, 3 rounds): the 29 side kernels (6-7 us each) add to the es2 contention.
-  bool ln_sums_side = [] {
-    const char* e = std::getenv("CAPGEN_LN_SUMS_SIDE");
-    return e && e[0] == '1';
-  }();
-  std::vector<LnBwd> lns_pending;
-  int lns_next = 0;
-  void lnb_block(LnBwd l, hipStream_t s) {
-    if (!ln_sums_side || es2 == s || (!l.dgamma && !l.dbias) || lns_next >= (int)a.lns.size() ||
-        (int64_t)l.M * l.d > a.lns_cap)  // (the image block's pair rows exceed a slot: in the kernel)
-      return lnb(l, s);
-    LnBwd side = l;
-    l.y_save = a.lns[lns_next++];
-    l.dgamma = l.dbeta = l.dbias = nullptr;
-    lnb(l, s);
-    side.dy = l.y_save;
-    side.mask = RowMask{};
-    lns_pending.push_back(side);
-  }
   void attf(AttnGeom g, void* o, float* probs, DType t, hipStream_t s) {
     g.prio = prio(s);
     if (stamp_on) g.stamp = stamp(s, "attn_fwd " + std::to_string(g.Lq) + "x" + std::to_string(g.Lk));
@@ -541,7 +511,6 @@ struct capgen_engine {
     p.take(a.grad_scale, 4);
     p.take(a.loss, 4);
     p.take(a.loss_ce, 4);
-    p.take(a.gEnc32, (size_t)Me * d);
     T_(a.gEnc, Me * d);
     p.take(a.rl_sample, Md);
     p.take(a.rl_lse, Md);
@@ -552,9 +521,6 @@ struct capgen_engine {
     p.take(a.rl_scal, 8);
     const int64_t dmax = std::max<int64_t>(std::max(d, dd), L_().dwe);
     T_(a.tmp, Mx * dmax);
-    a.lns.resize(ln_sums_side ? kLnSideSlots : 0);  // (~90 MB at C2: only for the CAPGEN_LN_SUMS_SIDE experiment)
-    for (auto& x : a.lns) T_(x, Mx * dmax);
-    a.lns_cap = ln_sums_side ? (int64_t)Mx * dmax : 0;
     T_(a.gOut, Mx * dmax);
     T_(a.gRes, Mx * dmax);
     T_(a.gKV, Me * L_().Ld * 2 * dd);
@@ -641,12 +607,6 @@ struct capgen_engine {
     Planner p;
     plan_acts(p, nB, nN, nT);
     CAPGEN_HIP(hipMalloc(&ws, p.used));
-    // diagnostic (CAPGEN_POISON=<byte>): fill the fresh activation workspace with that byte, so a
-    // read of a never-written element shows up deterministically (0xff: NaN in bf16 and f32)
-    if (const char* e = std::getenv("CAPGEN_POISON")) {
-      CAPGEN_HIP(hipMemset(ws, (int)std::strtol(e, nullptr, 0), p.used));
-      hz::host_sync(nullptr);
-    }
     Planner q;
     q.base = (char*)ws;
     plan_acts(q, nB, nN, nT);
@@ -890,17 +850,8 @@ struct capgen_engine {
     }
     for (int l = 0; l < L.Le; ++l)
       enc_layer_fwd(L.enc[l], a.enc[l], a.X[l], a.X[l + 1], B, N, cfg.encode_mask ? a.valid : nullptr, l, drop_on, s);
-    // cross-attention K/V of every decoder block in one GEMM over the encoder output; with
-    // kv_split block 0's slice first, the other blocks' on es2 beside decoder block 0
-    const bool kvs = kv_split && front && !cap_split && L.Ld > 1;
-    const int nkv0 = kvs ? 2 * dd : L.Ld * 2 * dd;
-    linear(a.X[L.Le], d, L.Wkv_all, d, a.KV, (int64_t)L.Ld * 2 * dd, act, Me, nkv0, d, nullptr, 0, s);
-    if (kvs) {
-      dep(s, es2, ev_ff);
-      linear(a.X[L.Le], d, L.Wkv_all + (int64_t)nkv0 * d, d, at(a.KV, nkv0), (int64_t)L.Ld * 2 * dd, act, Me,
-             (L.Ld - 1) * 2 * dd, d, nullptr, 0, es2);
-      hz::record(ev_kv, es2);
-    }
+    // cross-attention K/V of every decoder block in one GEMM over the encoder output
+    linear(a.X[L.Le], d, L.Wkv_all, d, a.KV, (int64_t)L.Ld * 2 * dd, act, Me, L.Ld * 2 * dd, d, nullptr, 0, s);
 
     // ---- decoder (model.py:419-459) ----
     if (front && cap_split) cap_cut(s, 2, s);
@@ -911,7 +862,6 @@ struct capgen_engine {
       const auto& w = L.dec[l];
       auto& A = a.dec[l];
       if (!(front && l == 0)) dec_self_half(l, a.tmp, s);
-      if (kvs && l == 1) hz::wait(s, ev_kv);
       // cross attention over the encoder output, context mask = region key-pad (model.py:82)
       AttnGeom c;
       c.B = B, c.H = Hd, c.Lq = Lq, c.Lk = N, c.dk = dkd;
@@ -1064,13 +1014,6 @@ struct capgen_engine {
     const char* e = std::getenv("CAPGEN_COLSUM_SIDE");
     return !(e && e[0] == '0');
   }();
-  // input-gradient partial products queued for es2 like the weight gradients (the encoder-output
-  // gradient per decoder block, split_enc_grad below); `mark`: record ev_part after this one
-  struct SideGemm {
-    GemmArgs ga;
-    bool mark;
-  };
-  std::vector<SideGemm> nn_pending;
   // es2 waits for everything issued on s so far, then runs the queued weight-gradient GEMMs
   void flush(hipStream_t s) {
     fork(s);
@@ -1078,22 +1021,7 @@ struct capgen_engine {
     dw_pending.clear();
     for (const ColJob& j : col_pending) column_sum(j.X, j.M, j.N, j.N, 1.f, nullptr, j.db, act, es2, NSTRIPE, n_small);
     col_pending.clear();
-    for (const LnBwd& l : lns_pending) layernorm_param_sums(l, act, es2);
-    lns_pending.clear();
-    for (const SideGemm& j : nn_pending) {
-      gemm(j.ga, act, DType::F32, false, true, es2);
-      if (j.mark) hz::record(ev_part, es2);
-    }
-    nn_pending.clear();
   }
-  // The gradient into the encoder output is sum_l gKV_l . Wkv_l over the decoder blocks' cross
-  // K/V (model.py:441-446 restated backward).  bf16 mode: block l's term (l >= 1) is accumulated
-  // into an f32 buffer on es2 as soon as block l's cross-attention backward has produced gKV_l
-  // (and its K/V weight gradient joins the block's grouped dW launch), so after the decoder only
-  // block 0's term is left on the critical stream -- one K = 2d GEMM whose epilogue adds the f32
-  // partial sum -- instead of one K = 2 d Ld GEMM.  Measured slower (3.45 vs 3.41 ms/step at
-  // C2: the side GEMMs queue behind the weight-gradient groups on es2 and the critical stream
-  // waits for them), so off unless CAPGEN_SPLIT_ENC_GRAD=1 (experiment knob)
   // Decoder block 0's self-attention half (and the decoder-embedding branch) on es2, concurrent
   // with the encoder chain: once block 0's cross-attention backward has produced its K/V
   // gradient, the encoder-output gradient (all blocks' gKV . Wkv_all) is complete, and nothing
@@ -1102,17 +1030,9 @@ struct capgen_engine {
     const char* e = std::getenv("CAPGEN_OVERLAP_FRONT");
     return !(e && e[0] == '0');
   }();
-  bool kv_split = [] {  // CAPGEN_KV_SPLIT=1: decoder blocks 1.. cross K/V GEMM on es2 (experiment)
-    const char* e = std::getenv("CAPGEN_KV_SPLIT");
-    return e && e[0] == '1';
-  }();
   bool overlap_dec0 = [] {
     const char* e = std::getenv("CAPGEN_OVERLAP_DEC0");
     return !(e && e[0] == '0');
-  }();
-  bool split_enc_grad = [] {
-    const char* e = std::getenv("CAPGEN_SPLIT_ENC_GRAD");
-    return e && e[0] == '1';
   }();
   // GemmArgs of dX[M,K] (+)= dY[M,N] . W[N,K] (linear_dx) without launching it
   GemmArgs dx_args(const void* dY, int64_t ldy, int64_t woff, int64_t ldw, void* dX, int64_t ldx, int M, int N,
@@ -1127,7 +1047,7 @@ struct capgen_engine {
   // X = block input, H = hidden activations.
   void ffn_bwd(int M, int d, int f, const LnBwd& lb, const void* X, const void* H, int64_t W1, int64_t b1, int64_t W2,
                void* gH, hipStream_t s) {
-    lnb_block(lb, s);
+    lnb(lb, s);
     void* gA = lb.d_a;
     dw_side(gA, d, H, f, W2, f, M, d, f, nullptr, s);
     const bool side = colsum_side && es2 != s;
@@ -1135,44 +1055,11 @@ struct capgen_engine {
     if (side) col_pending.push_back(ColJob{gH, M, f, GS(b1)});                           // db1 = colsum
     dw_side(gH, f, X, d, W1, d, M, f, d, nullptr, s);
     linear_dx(gH, f, W1, d, lb.d_res, d, M, f, d, 1, nullptr, nullptr, s);
-    flush_deferred(s);
-  }
-  // Deferred block flush (CAPGEN_FLUSH_DEFER, experiment): a transformer block's weight-gradient
-  // group and bucket update are issued after the NEXT block's FFN input gradients instead of at the
-  // block's end, so the side stream's largest launch (the block's grouped dW, 64 KB LDS and 16
-  // waves per CU) overlaps the latency-bound LayerNorm / attention / projection kernels rather than
-  // the FFN-down input gradient, the GEMM it slowed most (un-profiled timeline: 2304x2048x512 dX
-  // 29-39 us beside the group vs 13.4 us alone)
-  // Measured neutral (3-round A/B 3.048-3.067 vs 3.046-3.067 ms/step): the contention moves to the
-  // kernels the group then overlaps.  Off; CAPGEN_FLUSH_DEFER=1 enables.
-  bool flush_defer = [] {
-    const char* e = std::getenv("CAPGEN_FLUSH_DEFER");
-    return e && e[0] == '1';
-  }();
-  bool deferred = false;
-  int64_t deferred_off = 0, deferred_n = 0;
-  void defer_bucket(int64_t off, int64_t n, hipStream_t s) {
-    flush_deferred(s);
-    if (!flush_defer || es2 == s) return bucket(off, n, s);
-    deferred = true, deferred_off = off, deferred_n = n;
-  }
-  void flush_deferred(hipStream_t s) {
-    if (!deferred) return;
-    deferred = false;
-    bucket(deferred_off, deferred_n, s);
   }
   // MHA output projection + LayerNorm backward: lb as above (d_res = grad wrt the residual /
   // query input); writes grad wrt the attention output into gATT.
   void mha_out_bwd(int M, int d, const LnBwd& lb, const void* att, int64_t Wo, void* gATT, hipStream_t s) {
-    const bool snap = dbg_stop == 4 && dbg_snap_on;  // diagnostic snapshots (tools/bwd_bisect.py)
-    if (snap) {
-      CAPGEN_HIP(hipMemcpyAsync(dbg_snap[0], lb.dy, (size_t)M * d * es_(), hipMemcpyDeviceToDevice, s));
-      CAPGEN_HIP(hipMemcpyAsync(dbg_snap[2], lb.v, (size_t)M * d * es_(), hipMemcpyDeviceToDevice, s));
-      CAPGEN_HIP(hipMemcpyAsync(dbg_snap[3], lb.mean, (size_t)M * 4, hipMemcpyDeviceToDevice, s));
-      CAPGEN_HIP(hipMemcpyAsync(dbg_snap[4], lb.rstd, (size_t)M * 4, hipMemcpyDeviceToDevice, s));
-    }
-    lnb_block(lb, s);
-    if (snap) CAPGEN_HIP(hipMemcpyAsync(dbg_snap[1], lb.d_a, (size_t)M * d * es_(), hipMemcpyDeviceToDevice, s));
+    lnb(lb, s);
     dw_side(lb.d_a, d, att, d, Wo, d, M, d, d, nullptr, s);
     linear_dx(lb.d_a, d, Wo, d, gATT, d, M, d, d, 0, nullptr, nullptr, s);
   }
@@ -1201,43 +1088,6 @@ struct capgen_engine {
   // every producer of the bucket's gradients (consecutive buckets after one flush)
   // from_s: every producer of the bucket's gradients ran on s (no flush, ec waits for s)
   bool bstep = false;
-  // diagnostic: backward stops early (1: after the encoder-output gradient GEMM, 2: after the last
-  // encoder block's FFN backward, 3: after that whole block) so capgen_debug_copy_buffer can
-  // compare intermediate gradients run to run (tools/bwd_bisect.py)
-  void* dbg_snap[5] = {};  // stop 4: dy / d_a / v / mean / rstd of the last encoder block's MHA LayerNorm
-  // diagnostic (CAPGEN_DEBUG_ENC_SNAP=1): the encoder chain's gradient after the Wkv_all input
-  // gradient (slot Le) and after each encoder block's backward (slot l), copied on the critical
-  // stream -- capgen_debug_copy_buffer(16 + slot) -- to find the block where two runs part
-  std::vector<void*> dbg_enc;
-  size_t dbg_enc_bytes = 0;
-  bool dbg_enc_on = [] {
-    const char* e = std::getenv("CAPGEN_DEBUG_ENC_SNAP");
-    return e && e[0] == '1';
-  }();
-  void enc_snap(int slot, const void* src, size_t bytes, hipStream_t s) {
-    if (!dbg_enc_on) return;
-    if (dbg_enc.empty() || dbg_enc_bytes < bytes) {
-      hz::host_sync(nullptr);
-      for (void* q : dbg_enc) CAPGEN_HIP(hipFree(q));
-      dbg_enc.assign(2 * L.Le + 1, nullptr);  // + slot Le + 1 + l: block l's gR after the dX W1 accumulate
-      for (void*& q : dbg_enc) CAPGEN_HIP(hipMalloc(&q, bytes));
-      dbg_enc_bytes = bytes;
-    }
-    CAPGEN_HIP(hipMemcpyAsync(dbg_enc[slot], src, bytes, hipMemcpyDeviceToDevice, s));
-  }
-  // diagnostic (CAPGEN_DEBUG_ENC_CHAIN=1): every encoder block's gR (slot l) and block-input
-  // gradient (slot Le + l) in buffers of their own, readable after the call without in-run copies
-  std::vector<void*> dbg_chain;
-  void* dbg_eO = nullptr;  // the encoder chain's starting gradient (which = 13)
-  bool dbg_chain_on = [] {
-    const char* e = std::getenv("CAPGEN_DEBUG_ENC_CHAIN");
-    return e && e[0] == '1';
-  }();
-  bool dbg_snap_on = false;
-  int dbg_stop = [] {
-    const char* e = std::getenv("CAPGEN_DEBUG_BWD_STOP");
-    return e ? std::atoi(e) : 0;
-  }();
   // transformer blocks per gradient bucket (one flush = one event record on the critical stream)
   int bucket_blocks = [] {
     const char* e = std::getenv("CAPGEN_BUCKET_BLOCKS");
@@ -1298,12 +1148,9 @@ struct capgen_engine {
 
   // backward of enc_layer_fwd: gO = grad wrt Xout on entry, grad wrt X on exit; gR scratch
   void enc_layer_bwd(const EncLayerOff& w, EncAct& A, Acts::GradBufs& gb, const void* X, int B, int N,
-                     const uint8_t* valid, int layer, bool on, void* gO, void* gR, hipStream_t s,
-                     void* gO_out = nullptr) {
-    // gO_out (diagnostic, CAPGEN_DEBUG_ENC_CHAIN): the block-input gradient goes to its own buffer
-    // instead of overwriting gO in place
+                     const uint8_t* valid, int layer, bool on, void* gO, void* gR, hipStream_t s) {
     const int Me = B * N, d = L.d, He = L.He, dke = d / He;
-    void* go = gO_out ? gO_out : gO;
+    void* go = gO;
     const float p = cfg.dropout, pa = cfg.attention_dropout;
     RowMask mask{};
     mask.valid = valid;
@@ -1312,11 +1159,6 @@ struct capgen_engine {
     const LnBwd lmha = lnb_desc(Me, d, gR, A.v1, A.m1, A.r1, w.ln1g, w.ln1b, -1, RowMask{},
                                 mk_drop(p, site(0, layer, 1), on), go, gb.gA1);
     ffn_bwd(Me, d, L.fe, lffn, A.Y, A.H, w.W1, w.b1, w.W2, gb.gH, s);  // gR = grad wrt Y
-    if (layer >= 0 && layer < L.Le) enc_snap(L.Le + 1 + layer, gR, (size_t)Me * d * es_(), s);
-    if (dbg_stop == 2 && layer == L.Le - 1) return;
-    dbg_snap_on = layer == L.Le - 1;
-    if (dbg_stop == 4 && dbg_snap_on && !dbg_snap[0])
-      for (void*& q : dbg_snap) CAPGEN_HIP(hipMalloc(&q, (size_t)Me * d * es_()));
     AttnGeom g;
     g.B = B, g.H = He, g.Lq = N, g.Lk = N, g.dk = dke;
     g.q = A.qkv, g.q_ld = 3 * d, g.q_bs = (int64_t)N * 3 * d;
@@ -1327,7 +1169,6 @@ struct capgen_engine {
     g.temperature = std::sqrt((float)dke);
     g.drop = mk_drop(pa, site(0, layer, 0), on);
     mha_out_bwd(Me, d, lmha, A.att, w.Wo, gb.gATT1, s);
-    dbg_snap_on = false;
     attb(g, A.P, gb.gATT1, gb.gQKV, at(gb.gQKV, d), at(gb.gQKV, 2 * d), act, s);
     dw_side(gb.gQKV, 3 * d, X, d, w.Wqkv, d, Me, 3 * d, d, nullptr, s);
     linear_dx(gb.gQKV, 3 * d, w.Wqkv, d, go, d, Me, 3 * d, d, 1, nullptr, nullptr, s);  // gO = grad wrt X
@@ -1371,7 +1212,6 @@ struct capgen_engine {
     require(fB > 0, "backward: call forward first");
     grads_sharded = false;
     stamp_next = stamp_fwd_end;
-    deferred = false;  // (a diagnostic early return may have left one)
     const int B = fB, N = fN, Lq = fT - 1, Me = B * N, Md = B * Lq, d = L.d, dd = L.dd;
     const int He = L.He, Hd = L.Hd, dke = d / He, dkd = dd / Hd;
     const bool on = fwd_drop;
@@ -1399,8 +1239,6 @@ struct capgen_engine {
       adam_prepare(step, cfg.lr, cfg.beta1, cfg.beta2, adam_scal, cst == hipStreamCaptureStatusNone ? ec : s);
       zbuckets.clear();
     }
-    lns_next = 0;
-    lns_pending.clear();
 
     RowMask dmask{};
     dmask.ids = a.ids, dmask.pad_idx = cfg.pad_idx;
@@ -1439,7 +1277,6 @@ struct capgen_engine {
     bucket(L.Wc, L.n_dense - L.Wc, s);  // flushed after the dX GEMM above: it reads Wc
 
     const int64_t kvld = (int64_t)L.Ld * 2 * dd;
-    const bool split_kv = split_enc_grad && act == DType::BF16 && es2 != s && L.Ld > 1;
     void* gO = a.gOut;
     void* gR = a.gRes;
     if (L.has_mf) {  // gRes = grad wrt D[Ld]; a.mfGU = grad wrt U (its encoder part is added below)
@@ -1463,14 +1300,6 @@ struct capgen_engine {
       c.drop = mk_drop(pa, site(1, l, 5), on);
       mha_out_bwd(Md, dd, lcross, A.attc, w.Wo_c, gb.gATT2, s);  // gO = grad wrt D1 (residual part)
       attb(c, A.Pc, gb.gATT2, gb.gQc, at(a.gKV, (int64_t)l * 2 * dd), at(a.gKV, (int64_t)l * 2 * dd + dd), act, s);
-      if (split_kv) {  // this block's cross K/V: weight gradient and (l >= 1) encoder-output term
-        dw_side(at(a.gKV, (int64_t)l * 2 * dd), kvld, a.X[L.Le], d, L.Wkv_all + (int64_t)l * 2 * dd * d, d, Me,
-                2 * dd, d, nullptr, s);
-        if (l >= 1)
-          nn_pending.push_back(SideGemm{dx_args(at(a.gKV, (int64_t)l * 2 * dd), kvld, L.Wkv_all + (int64_t)l * 2 * dd * d,
-                                                d, a.gEnc32, d, Me, 2 * dd, d, l != L.Ld - 1),
-                                        l == 1});
-      }
       // block 0: the rest of the block runs on es2 (ov), the encoder chain starts on s below
       const bool ov = l == 0 && overlap_dec0 && es2 != s;
       const hipStream_t hs = ov ? es2 : s;
@@ -1492,7 +1321,7 @@ struct capgen_engine {
       linear_dx(gb.gQKV, 3 * dd, w.Wqkv, dd, gR, dd, Md, 3 * dd, dd, 1, nullptr, nullptr, hs);
       if (l % bucket_blocks == 0)  // blocks l .. l + bucket_blocks - 1 (contiguous in the arena)
         (ov || l == 0 ? bucket(w.Wqkv, dec_end(std::min(l + bucket_blocks - 1, L.Ld - 1)) - w.Wqkv, hs)
-                      : defer_bucket(w.Wqkv, dec_end(std::min(l + bucket_blocks - 1, L.Ld - 1)) - w.Wqkv, hs));
+                      : bucket(w.Wqkv, dec_end(std::min(l + bucket_blocks - 1, L.Ld - 1)) - w.Wqkv, hs));
       if (ov) dec0_on_side = true;
       std::swap(gO, gR);  // gO = grad wrt D_l
     }
@@ -1517,21 +1346,10 @@ struct capgen_engine {
     // the encoder chain must not overwrite gO (read by the decoder-embedding branch on es2):
     // it runs on the other residual buffer and on tmp (free during backward)
     gO = eO;
-    dbg_eO = eO;
     gR = a.tmp;
-    if (split_kv) {  // block 0's term + the f32 sum of blocks Ld-1 .. 1 (summed on es2)
-      hz::wait(s, ev_part);
-      GemmArgs ga = dx_args(a.gKV, kvld, L.Wkv_all, d, gO, d, Me, 2 * dd, d, 0);
-      ga.cin = a.gEnc32, ga.ldcin = d, ga.prio = prio(s);
-      if (stamp_on) ga.stamp = stamp(s, "gemm dX " + dims(Me, d, 2 * dd));
-      gemm(ga, act, act, false, true, s);
-    } else {
-      linear_dx(a.gKV, kvld, L.Wkv_all, d, gO, d, Me, L.Ld * 2 * dd, d, 0, nullptr, nullptr, s);
-    }
-    enc_snap(L.Le, gO, (size_t)Me * d * es_(), s);
-    if (dbg_stop == 1) return join(s);  // diagnostic (CAPGEN_DEBUG_BWD_STOP): capgen_debug_copy_buffer
+    linear_dx(a.gKV, kvld, L.Wkv_all, d, gO, d, Me, L.Ld * 2 * dd, d, 0, nullptr, nullptr, s);
     if (L.has_mf) first_region_grad(a.mfGU, B, Lq, N, d, gO, act, s);  // enc[:, 0] of U = D + enc[:, 0]
-    if (!split_kv) dw_side(a.gKV, kvld, a.X[L.Le], d, L.Wkv_all, d, Me, L.Ld * 2 * dd, d, nullptr, s);
+    dw_side(a.gKV, kvld, a.X[L.Le], d, L.Wkv_all, d, Me, L.Ld * 2 * dd, d, nullptr, s);
     // the decoder-embedding branch (es2) has been issued: every decoder-side gradient is final
     // the flush of the first bucket follows the dX GEMM above (it reads Wkv_all); es2 then holds
     // every producer of the other three buckets
@@ -1539,24 +1357,12 @@ struct capgen_engine {
     bucket(L.Wel, L.dec[0].Wqkv - L.Wel, s, false);       // word-embedding projection
     bucket(L.emb, L.enc_lng - L.emb, s, false);           // word embedding table
     bucket(L.dec_lng, L.total - L.dec_lng, s, false);     // decoder LN / biases, classifier bias
-    if (dbg_chain_on && dbg_chain.empty()) {
-      hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-      CAPGEN_HIP(hipStreamIsCapturing(s, &st));
-      require(st == hipStreamCaptureStatusNone, "CAPGEN_DEBUG_ENC_CHAIN: first backward must be eager");
-      dbg_chain.assign(2 * L.Le, nullptr);
-      for (void*& q : dbg_chain) CAPGEN_HIP(hipMalloc(&q, (size_t)Me * d * es_()));
-    }
     for (int l = L.Le - 1; l >= 0; --l) {
       const auto& w = L.enc[l];
-      void* const gRl = dbg_chain_on ? dbg_chain[l] : gR;
-      void* const gOl = dbg_chain_on ? dbg_chain[L.Le + l] : nullptr;
-      enc_layer_bwd(w, a.enc[l], a.genc[l], a.X[l], B, N, cfg.encode_mask ? a.valid : nullptr, l, on, gO, gRl, s, gOl);
-      if (gOl) gO = gOl;
-      enc_snap(l, gO, (size_t)Me * d * es_(), s);
-      if (dbg_stop >= 2 && l == L.Le - 1) return join(s);  // 3, 4: after the whole block
+      enc_layer_bwd(w, a.enc[l], a.genc[l], a.X[l], B, N, cfg.encode_mask ? a.valid : nullptr, l, on, gO, gR, s);
       if (l % bucket_blocks == 0)
         (l == 0 ? bucket(w.Wqkv, enc_end(std::min(l + bucket_blocks - 1, L.Le - 1)) - w.Wqkv, s)
-                : defer_bucket(w.Wqkv, enc_end(std::min(l + bucket_blocks - 1, L.Le - 1)) - w.Wqkv, s));
+                : bucket(w.Wqkv, enc_end(std::min(l + bucket_blocks - 1, L.Le - 1)) - w.Wqkv, s));
     }
     // the tail of the step's dependency chain: the encoder-embedding LayerNorm backward and
     // weight gradient, then its Adam, which the next forward's first GEMM needs -- on the
@@ -2058,8 +1864,6 @@ struct capgen_engine {
   ~capgen_engine() {
     if (es) (void)hipStreamSynchronize(es);
     drop_graph();
-    for (void* q : dbg_enc) (void)hipFree(q);
-    for (void* q : dbg_chain) (void)hipFree(q);
     if (comm) ncclCommDestroy(comm);
     for (void* p : {(void*)params, (void*)grads, (void*)am, (void*)av, (void*)shadow, (void*)pe, (void*)step,
                     (void*)adam_scal, (void*)seed, (void*)scalars, (void*)gstripe, ws, gws, (void*)stamp_ring})
@@ -2069,7 +1873,7 @@ struct capgen_engine {
     if (ev_out) (void)hipEventDestroy(ev_out);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
-    for (hipEvent_t e : {ev_b1, ev_b2, ev_cj, ev_count, ev_part, ev_ff, ev_fj, ev_kv})
+    for (hipEvent_t e : {ev_b1, ev_b2, ev_cj, ev_count, ev_ff, ev_fj})
       if (e) (void)hipEventDestroy(e);
     if (ec && ec != es && ec != es2) (void)hipStreamSynchronize(ec), (void)hipStreamDestroy(ec);
     if (es2 && es2 != es) (void)hipStreamSynchronize(es2), (void)hipStreamDestroy(es2);
@@ -2168,7 +1972,7 @@ int capgen_create(const capgen_config* cfg, int device, capgen_t** out) {
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
     if (nstreams >= 3) CAPGEN_HIP(hipStreamCreateWithFlags(&h->ec, hipStreamNonBlocking));
     else h->ec = h->es2;
-    for (hipEvent_t* e : {&h->ev_b1, &h->ev_b2, &h->ev_cj, &h->ev_part, &h->ev_ff, &h->ev_fj, &h->ev_kv})
+    for (hipEvent_t* e : {&h->ev_b1, &h->ev_b2, &h->ev_cj, &h->ev_ff, &h->ev_fj})
       CAPGEN_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_count, hipEventDisableTiming));
@@ -2486,6 +2290,9 @@ int capgen_debug_gemm_variant(int v) {
 int capgen_debug_ffn_persist(int M, int d, int fe, const void* X, const void* W1, const float* b1, const void* W2,
                              void* H, void* Y, int grid, int acquire, void* stream) {
   return guarded([&] {
+    // opt-in: an experiment kernel, not on the product path (CAPGEN_PERSIST_OK=1)
+    const char* ok = std::getenv("CAPGEN_PERSIST_OK");
+    require(ok && ok[0] == '1', "capgen_debug_ffn_persist: experiment hook, set CAPGEN_PERSIST_OK=1 to run it");
     gemm_init();
     GemmArgs g1, g2;
     g1.M = M, g1.N = fe, g1.K = d, g1.A = X, g1.lda = d, g1.B = W1, g1.ldb = d, g1.C = H, g1.ldc = fe, g1.bias = b1;
@@ -2506,9 +2313,6 @@ int capgen_debug_copy_buffer(capgen_t* h, int which, void* host_dst, int64_t byt
     void* src = which == 0 ? h->a.tmp : which == 1 ? h->a.gOut : which == 2 ? h->a.gRes : which == 3 ? h->a.gKV
               : which == 4 ? h->a.genc[Le - 1].gH : which == 5 ? h->a.genc[Le - 1].gAf
               : which == 6 ? h->a.genc[Le - 1].gA1 : which == 7 ? h->a.genc[Le - 1].gQKV
-              : which >= 8 && which < 13 ? h->dbg_snap[which - 8]
-              : which == 13 ? h->dbg_eO
-              : which >= 16 && which - 16 < (int)h->dbg_enc.size() ? h->dbg_enc[which - 16]
               // 32 + 8 l + j: encoder block l's per-block gradient buffers (never overwritten later in
               // the backward): j = 0 gAf, 1 gH, 2 gA1, 3 gATT1, 4 gQKV
               : which >= 32 && (which - 32) / 8 < Le && (which - 32) % 8 < 5
@@ -2527,11 +2331,8 @@ int capgen_debug_copy_buffer(capgen_t* h, int which, void* host_dst, int64_t byt
                      : (which - 128) % 8 == 5 ? h->a.enc[(which - 128) / 8].v2
                      : (which - 128) % 8 == 6 ? (void*)h->a.enc[(which - 128) / 8].m2
                                              : (void*)h->a.enc[(which - 128) / 8].r2)
-              // 96 + l: block l's gR, 112 + l: block l's input gradient (CAPGEN_DEBUG_ENC_CHAIN=1)
-              : which >= 96 && which < 96 + Le && !h->dbg_chain.empty() ? h->dbg_chain[which - 96]
-              : which >= 112 && which < 112 + Le && !h->dbg_chain.empty() ? h->dbg_chain[Le + which - 112]
                   : nullptr;
-    require(src != nullptr, "debug_copy_buffer: which in 0..12 (8-12 need CAPGEN_DEBUG_BWD_STOP=4)");
+    require(src != nullptr, "debug_copy_buffer: which in 0..7, 32 + 8 l + 0..4, 80 + 0..Le, 128 + 8 l + 0..7");
     hz::host_sync(nullptr);
     CAPGEN_HIP(hipMemcpy(host_dst, src, (size_t)bytes, hipMemcpyDeviceToHost));
   });

@@ -323,40 +323,6 @@ static bool tune_cold() {
   }();
   return on;
 }
-// CAPGEN_TUNE_BG=1 (experiment): each timed candidate runs beside a background stream kernel
-// shaped like the step's bucket Adam (one 256-thread workgroup per CU streaming 96 MB read +
-// write), so the ranking sees the contention the step's critical GEMMs run under
-__global__ void tune_bg_kernel(const float4* __restrict__ a, float4* __restrict__ b, size_t n) {
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    float4 v = a[i];
-    v.x += 1.f;
-    b[i] = v;
-  }
-}
-static bool tune_bg() {
-  static const bool on = [] {
-    const char* e = std::getenv("CAPGEN_TUNE_BG");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-static void tune_bg_launch(hipStream_t s) {
-  static hipStream_t bg = nullptr;
-  static float4* buf = nullptr;
-  constexpr size_t kN = (48u << 20) / 16;  // 48 MB in, 48 MB out
-  if (!bg) {
-    CAPGEN_HIP(hipStreamCreateWithFlags(&bg, hipStreamNonBlocking));
-    CAPGEN_HIP(hipMalloc(&buf, 2 * kN * sizeof(float4)));
-    CAPGEN_HIP(hipMemset(buf, 0, 2 * kN * sizeof(float4)));
-    CAPGEN_HIP(hipDeviceSynchronize());
-  }
-  CAPGEN_HIP(hipStreamSynchronize(s));  // the scrub is done: background and candidate start together
-  tune_bg_kernel<<<256, 256, 0, bg>>>(buf, buf + kN, kN);
-}
-static void tune_bg_wait() {
-  CAPGEN_HIP(hipDeviceSynchronize());
-}
-
 template <typename F>
 static float tune_time(F&& launch, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   launch();  // warm-up (code, TLB)
@@ -378,12 +344,10 @@ static float tune_time(F&& launch, hipStream_t s, hipEvent_t e0, hipEvent_t e1) 
   float tot = 0.f;
   for (int r = 0; r < 3; ++r) {
     CAPGEN_HIP(hipMemsetAsync(buf, r, kScrub, s));
-    if (tune_bg()) tune_bg_launch(s);
     CAPGEN_HIP(hipEventRecord(e0, s));
     launch();
     CAPGEN_HIP(hipEventRecord(e1, s));
     CAPGEN_HIP(hipEventSynchronize(e1));
-    if (tune_bg()) tune_bg_wait();
     float ms = 0.f;
     CAPGEN_HIP(hipEventElapsedTime(&ms, e0, e1));
     tot += ms;
@@ -508,22 +472,6 @@ static void launch_bf16_tiles(const GemmArgs& g, hipStream_t s) {
       CAPGEN_HIP(hipStreamIsCapturing(s, &st));
       if (st == hipStreamCaptureStatusNone) ensure_ws(s, bytes);
       else c.splitk = 1;  // no allocation inside a capture
-    }
-  }
-  // diagnostic (CAPGEN_NO_KG=1): a k-group variant runs as its one-group tile with grid split-K =
-  // KG -- the same partial sums in the same order (bit-identical by construction, gemm_tile)
-  static const bool no_kg = [] {
-    const char* e = std::getenv("CAPGEN_NO_KG");
-    return e && e[0] == '1';
-  }();
-  if (no_kg && kVariantKG[c.variant] > 1 && c.splitk == 1) {
-    static const int base[NVARIANTS + 1] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
-                                            0, 0, 0, 0, 0, 0, 0, 6, 7, 21, 6, 17, 4, 5, 17};
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    CAPGEN_HIP(hipStreamIsCapturing(s, &st));
-    if (st == hipStreamCaptureStatusNone) {
-      c.splitk = kVariantKG[c.variant], c.variant = base[c.variant];
-      ensure_ws(s, splitk_bytes(g, c.splitk));
     }
   }
   launch_variant<TO, TA, TB>(c.variant, g, s, c.splitk);
@@ -757,8 +705,10 @@ int gemm_tune_load(const char* path) {
       const char* p = line + 1;
       int x, used = 0;
       while (std::sscanf(p, "%d%n", &x, &used) == 1) v.push_back(x), p += used;
-      if (v.size() >= 5 && v.size() == 4 + 3 * (size_t)v[3] + 1) {
-        const int var = v.back();
+      const bool grouped_variant =
+          v.size() >= 5 && std::find(std::begin(kGroupVariants), std::end(kGroupVariants), v.back()) != std::end(kGroupVariants);
+      if (grouped_variant && v[3] >= 1 && v[3] <= kMaxGroup && v.size() == 4 + 3 * (size_t)v[3] + 1) {
+        const int var = v.back();  // (a stale or corrupt variant is skipped: the group is tuned again)
         std::vector<int> key{v[0], v[1], v[2]};
         key.insert(key.end(), v.begin() + 4, v.end() - 1);
         g_group_tuned.emplace(key, var);
@@ -780,14 +730,16 @@ int gemm_tune_save(const char* path) {
   for (auto& kv : g_tuned) {
     const TuneKey& k = kv.first;
     std::fprintf(f, "g %d %d %d %d %d %d %d %d  # %s\n", k.M, k.N, k.K, k.ta, k.tb, k.out, kv.second.variant,
-                 kv.second.splitk, kVariantName[kv.second.variant]);
+                 kv.second.splitk,
+                 kv.second.variant >= 0 && kv.second.variant <= NVARIANTS ? kVariantName[kv.second.variant] : "?");
     ++n;
   }
   for (auto& kv : g_group_tuned) {
     const std::vector<int>& k = kv.first;
     std::fprintf(f, "G %d %d %d %d", k[0], k[1], k[2], (int)(k.size() - 3) / 3);
     for (size_t i = 3; i < k.size(); ++i) std::fprintf(f, " %d", k[i]);
-    std::fprintf(f, " %d  # %s\n", kv.second, kVariantName[kv.second]);
+    std::fprintf(f, " %d  # %s\n", kv.second,
+                 kv.second >= 0 && kv.second <= NVARIANTS ? kVariantName[kv.second] : "?");
     ++n;
   }
   std::fclose(f);

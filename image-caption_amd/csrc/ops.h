@@ -45,18 +45,10 @@ struct LnBwd {
   // contention relief: workgroup w accumulates into dgamma/dbeta/dbias + (w % stripes) * stripe_stride
   int stripes = 1;
   int64_t stripe_stride = 0;
-  void* y_save = nullptr;  // optional: the masked output gradient dy * rowmask (T), for layernorm_param_sums
   uint64_t* stamp = nullptr;  // diagnostic timestamps (StampScope)
   int wt = -1;                // write-through (sc1) d_res / d_a stores: 1/0, -1 = wt_default()
-  int coh = -1;  // diagnostic (CAPGEN_LNB_COH): bit 0 system-scope loads of mean / rstd, bit 1 of dy / v,
-                // bit 2 one full wait after the row loads
 };
 void layernorm_bwd(const LnBwd& a, DType t, hipStream_t s);
-// The LayerNorm parameter sums alone -- dgamma += sum y * xhat, dbeta += sum y, dbias += sum d_a --
-// from a.dy = the y_save of a layernorm_bwd run without sums (a.mask ignored: y is masked) and
-// its d_a: the critical-path kernel skips its per-workgroup reduction and atomics, this one runs
-// on the side stream.
-void layernorm_param_sums(const LnBwd& a, DType t, hipStream_t s);
 
 // out[m] = [feats[m] | pos[m] | 0] (width Kp), valid[m] = any(pos[m] != 0)  (model.py:202-209)
 // img_idx (optional, [M/N]): rows of image img_idx[b] of a resident [n_img, N, F] / [.., P] store

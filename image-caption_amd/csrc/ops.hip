@@ -102,105 +102,99 @@ __global__ void __launch_bounds__(LN_THREADS) ln_fwd_kernel(LnFwd a) {
   }
 }
 
-template <typename T, int DPL, int R, int NT = LN_THREADS>  // R rows in flight per wave: every load of them is issued first
+struct LnDummy {
+  uint64_t seed;
+  int32_t id;
+  uint8_t valid;
+};
+__device__ LnDummy g_ln_dummy = {0, 0, 1};
+
+// One row per wave.  The row index is wave-uniform (readfirstlane), so the row statistics, the row
+// mask and the dropout seed are scalar loads, issued together with the row's two 16-B vector loads
+// (dy, v) and gamma before any use: one memory round trip per row.
+//
+// (Round 3 ran R = 2 rows per wave -- both rows' loads first -- and, under co-scheduling with the
+// side streams, sometimes wrote the row it computed last shifted by a row-scalar-sized amount while
+// every input was equal after the call: 12-14 of 30 two-engine comparisons, 0 of 30 at one row.
+// Its ISA did not issue the loads together: hipcc drained row 0's dy / v loads with vmcnt(0)
+// before loading mean / rstd as per-lane vector loads, then issued row 1's.  The mechanism was not
+// isolated; the multi-row variant is deleted, not configured away.)
+template <typename T, int DPL, int NT = LN_THREADS>
 __global__ void __launch_bounds__(NT) ln_bwd_kernel(LnBwd a) {
   __shared__ float red[3][NT / 64][64 * DPL];
   StampScope stamp_scope(a.stamp);
   if (a.prio) __builtin_amdgcn_s_setprio(3);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int d = a.d, c0 = lane * DPL;
-  float dg[DPL], db[DPL], dz[DPL], gm[DPL];
+  const int m = blockIdx.x * (NT / 64) + wave;  // wave-uniform
+  const bool on = m < a.M;
+  const int64_t base = (int64_t)m * d + c0;
+  float gm[DPL], dy[DPL], v[DPL];
+  float mean = 0.f, rstd = 0.f;
+  int idv = 0, vld = 1;
+  // optional inputs are read through a pointer select (absent -> a device dummy), never inside a
+  // branch: a load in a branch makes hipcc wait for it at the join, one more round trip each
+  const uint64_t* seed_p = a.drop.seed_ptr ? a.drop.seed_ptr : &g_ln_dummy.seed;
+  const int32_t* ids_p = a.mask.ids ? a.mask.ids + (int64_t)min(m, a.M - 1) * a.mask.ids_ld : &g_ln_dummy.id;
+  const uint8_t* val_p = a.mask.valid ? a.mask.valid + min(m, a.M - 1) : &g_ln_dummy.valid;
+  const uint64_t seed_v = *seed_p;
+  const int idv_v = *ids_p;
+  const int vld_v = *val_p;
   load_f<float, DPL>(a.gamma + c0, gm);
+  if (on) {
+    load_f<T, DPL>(reinterpret_cast<const T*>(a.dy) + base, dy);
+    load_f<T, DPL>(reinterpret_cast<const T*>(a.v) + base, v);
+    mean = a.mean[m], rstd = a.rstd[m];
+  }
+  const uint64_t seed = a.drop.seed_ptr ? seed_v : 0;
+  if (a.mask.ids) idv = idv_v;
+  if (a.mask.valid) vld = vld_v;
+  const bool kept = !(a.mask.ids && idv == a.mask.pad_idx) && vld != 0;
+  float dg[DPL], db[DPL], dz[DPL];
 #pragma unroll
   for (int e = 0; e < DPL; ++e) dg[e] = db[e] = dz[e] = 0.f;
-  const uint64_t seed = a.drop.seed_ptr ? *a.drop.seed_ptr : 0;
-  const int stride = gridDim.x * (NT / 64);
-  for (int m0 = blockIdx.x * (NT / 64) + wave; m0 < a.M; m0 += R * stride) {
-    float dy[R][DPL], v[R][DPL], mean[R], rstd[R];
-    bool on[R], kept[R];
+  if (on) {
+    const float keep = kept ? 1.f : 0.f;
+    float g[DPL], xh[DPL], s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int u = 0; u < R; ++u) {  // every load of both rows (row mask included) first
-      const int m = m0 + u * stride;
-      on[u] = m < a.M;
-      if (on[u]) {
-        const int64_t base = (int64_t)m * d + c0;
-        if constexpr (sizeof(T) == 2 && DPL % 2 == 0) {
-          if (a.coh & 2) {  // diagnostic: system-scope (sc0 sc1) loads of the row inputs
-            const uint32_t* py = reinterpret_cast<const uint32_t*>(reinterpret_cast<const T*>(a.dy) + base);
-            const uint32_t* pv = reinterpret_cast<const uint32_t*>(reinterpret_cast<const T*>(a.v) + base);
+    for (int e = 0; e < DPL; ++e) {
+      const float y = dy[e] * keep;
+      xh[e] = (v[e] - mean) * rstd;
+      g[e] = y * gm[e];
+      s1 += g[e];
+      s2 = fmaf(g[e], xh[e], s2);
+      dg[e] = y * xh[e];
+      db[e] = y;
+    }
+    const float mg = wave_sum(s1) / (float)d, mgx = wave_sum(s2) / (float)d;
+    float dv[DPL];
 #pragma unroll
-            for (int e = 0; e < DPL / 2; ++e) {
-              const uint32_t wy = __hip_atomic_load(py + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              const uint32_t wv = __hip_atomic_load(pv + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              dy[u][2 * e] = __uint_as_float(wy << 16), dy[u][2 * e + 1] = __uint_as_float(wy & 0xffff0000u);
-              v[u][2 * e] = __uint_as_float(wv << 16), v[u][2 * e + 1] = __uint_as_float(wv & 0xffff0000u);
-            }
-          } else {
-            load_f<T, DPL>(reinterpret_cast<const T*>(a.dy) + base, dy[u]);
-            load_f<T, DPL>(reinterpret_cast<const T*>(a.v) + base, v[u]);
-          }
-        } else {
-          load_f<T, DPL>(reinterpret_cast<const T*>(a.dy) + base, dy[u]);
-          load_f<T, DPL>(reinterpret_cast<const T*>(a.v) + base, v[u]);
-        }
-        if (a.coh & 1) {  // diagnostic: system-scope (sc0 sc1) loads of the row statistics
-          mean[u] = __hip_atomic_load(a.mean + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          rstd[u] = __hip_atomic_load(a.rstd + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        } else {
-          mean[u] = a.mean[m], rstd[u] = a.rstd[m];
-        }
-        kept[u] = row_kept(a.mask, m);
+    for (int e = 0; e < DPL; ++e) dv[e] = rstd * (g[e] - mg - xh[e] * mgx);
+    constexpr bool whole = DPL * sizeof(T) % 16 == 0;
+    const bool wt = whole && a.wt > 0;
+    if (a.d_res) {
+      if constexpr (whole) {
+        if (wt) store_wt<T, DPL>(wt_rsrc(a.d_res), (uint32_t)(base * (int64_t)sizeof(T)), dv);
+        else store_f<T, DPL>(reinterpret_cast<T*>(a.d_res) + base, dv);
+      } else {
+        store_f<T, DPL>(reinterpret_cast<T*>(a.d_res) + base, dv);
       }
     }
-    if (a.coh & 4) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // diagnostic: no partial waits
+    if (a.d_a) {
+      if (a.drop.seed_ptr) {
 #pragma unroll
-    for (int u = 0; u < R; ++u) {
-      if (!on[u]) continue;
-      const int m = m0 + u * stride;
-      const int64_t base = (int64_t)m * d + c0;
-      const float keep = kept[u] ? 1.f : 0.f;
-      float g[DPL], xh[DPL], yv[DPL], s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int e = 0; e < DPL; ++e) {
-        const float y = dy[u][e] * keep;
-        yv[e] = y;
-        xh[e] = (v[u][e] - mean[u]) * rstd[u];
-        g[e] = y * gm[e];
-        s1 += g[e];
-        s2 = fmaf(g[e], xh[e], s2);
-        dg[e] = fmaf(y, xh[e], dg[e]);
-        db[e] += y;
+        for (int e = 0; e < DPL; ++e)
+          dv[e] = drop_keep(seed, a.drop.site, (uint32_t)(base + e), a.drop.thresh) ? dv[e] * a.drop.scale : 0.f;
       }
-      if (a.y_save) store_f<T, DPL>(reinterpret_cast<T*>(a.y_save) + base, yv);
-      const float mg = wave_sum(s1) / (float)d, mgx = wave_sum(s2) / (float)d;
-      float dv[DPL];
-#pragma unroll
-      for (int e = 0; e < DPL; ++e) dv[e] = rstd[u] * (g[e] - mg - xh[e] * mgx);
-      constexpr bool whole = DPL * sizeof(T) % 16 == 0;
-      const bool wt = whole && a.wt > 0;
-      if (a.d_res) {
-        if constexpr (whole) {
-          if (wt) store_wt<T, DPL>(wt_rsrc(a.d_res), (uint32_t)(base * (int64_t)sizeof(T)), dv);
-          else store_f<T, DPL>(reinterpret_cast<T*>(a.d_res) + base, dv);
-        } else {
-          store_f<T, DPL>(reinterpret_cast<T*>(a.d_res) + base, dv);
-        }
+      if constexpr (whole) {
+        if (wt) store_wt<T, DPL>(wt_rsrc(a.d_a), (uint32_t)(base * (int64_t)sizeof(T)), dv);
+        else store_f<T, DPL>(reinterpret_cast<T*>(a.d_a) + base, dv);
+      } else {
+        store_f<T, DPL>(reinterpret_cast<T*>(a.d_a) + base, dv);
       }
-      if (a.d_a) {
-        if (a.drop.seed_ptr) {
 #pragma unroll
-          for (int e = 0; e < DPL; ++e)
-            dv[e] = drop_keep(seed, a.drop.site, (uint32_t)(base + e), a.drop.thresh) ? dv[e] * a.drop.scale : 0.f;
-        }
-        if constexpr (whole) {
-          if (wt) store_wt<T, DPL>(wt_rsrc(a.d_a), (uint32_t)(base * (int64_t)sizeof(T)), dv);
-          else store_f<T, DPL>(reinterpret_cast<T*>(a.d_a) + base, dv);
-        } else {
-          store_f<T, DPL>(reinterpret_cast<T*>(a.d_a) + base, dv);
-        }
-#pragma unroll
-        for (int e = 0; e < DPL; ++e) dz[e] += dv[e];
-      }
+      for (int e = 0; e < DPL; ++e) dz[e] = dv[e];
     }
   }
   if (!a.dgamma && !a.dbias) return;
@@ -226,81 +220,6 @@ __global__ void __launch_bounds__(NT) ln_bwd_kernel(LnBwd a) {
     }
     if (a.dbias) atomicAdd(a.dbias + so + c, sz);
   }
-}
-
-// LayerNorm parameter sums on the side stream (layernorm_param_sums): the same per-workgroup
-// reduction and striped atomics as ln_bwd_kernel's tail, from y = dy * rowmask (saved by the
-// critical-path kernel), the saved LN input / statistics and d_a
-template <typename T, int DPL>
-__global__ void __launch_bounds__(LN_THREADS) ln_sums_kernel(LnBwd a) {
-  __shared__ float red[3][LN_THREADS / 64][64 * DPL];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int d = a.d, c0 = lane * DPL;
-  float dg[DPL], db[DPL], dz[DPL];
-#pragma unroll
-  for (int e = 0; e < DPL; ++e) dg[e] = db[e] = dz[e] = 0.f;
-  for (int m = blockIdx.x * (LN_THREADS / 64) + wave; m < a.M; m += gridDim.x * (LN_THREADS / 64)) {
-    const int64_t base = (int64_t)m * d + c0;
-    float y[DPL], v[DPL], z[DPL];
-    load_f<T, DPL>(reinterpret_cast<const T*>(a.dy) + base, y);
-    load_f<T, DPL>(reinterpret_cast<const T*>(a.v) + base, v);
-    if (a.dbias) load_f<T, DPL>(reinterpret_cast<const T*>(a.d_a) + base, z);
-    const float mean = a.mean[m], rstd = a.rstd[m];
-#pragma unroll
-    for (int e = 0; e < DPL; ++e) {
-      dg[e] = fmaf(y[e], (v[e] - mean) * rstd, dg[e]);
-      db[e] += y[e];
-      if (a.dbias) dz[e] += z[e];
-    }
-  }
-  const int64_t so = (int64_t)(blockIdx.x % a.stripes) * a.stripe_stride;
-#pragma unroll
-  for (int e = 0; e < DPL; ++e) {
-    red[0][wave][c0 + e] = dg[e];
-    red[1][wave][c0 + e] = db[e];
-    red[2][wave][c0 + e] = dz[e];
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < d; c += LN_THREADS) {
-    float sg = 0.f, sb = 0.f, sz = 0.f;
-#pragma unroll
-    for (int w = 0; w < LN_THREADS / 64; ++w) {
-      sg += red[0][w][c];
-      sb += red[1][w][c];
-      sz += red[2][w][c];
-    }
-    if (a.dgamma) {
-      atomicAdd(a.dgamma + so + c, sg);
-      atomicAdd(a.dbeta + so + c, sb);
-    }
-    if (a.dbias) atomicAdd(a.dbias + so + c, sz);
-  }
-}
-template <typename T>
-static void ln_sums_dispatch(const LnBwd& a, hipStream_t s) {
-  dim3 grid(std::min(256, (a.M + 7) / 8));
-  switch (a.d / 64) {
-    case 1: ln_sums_kernel<T, 1><<<grid, LN_THREADS, 0, s>>>(a); break;
-    case 2: ln_sums_kernel<T, 2><<<grid, LN_THREADS, 0, s>>>(a); break;
-    case 4: ln_sums_kernel<T, 4><<<grid, LN_THREADS, 0, s>>>(a); break;
-    case 8: ln_sums_kernel<T, 8><<<grid, LN_THREADS, 0, s>>>(a); break;
-    case 16: ln_sums_kernel<T, 16><<<grid, LN_THREADS, 0, s>>>(a); break;
-    default: throw Error("layernorm: width must be 64 * {1,2,4,8,16}");
-  }
-}
-void layernorm_param_sums(const LnBwd& a, DType t, hipStream_t s) {
-  if (a.M <= 0 || (skip_mask() & 128) || (!a.dgamma && !a.dbias)) return;
-  require(a.dy && a.v && a.mean && a.rstd && (!a.dbias || a.d_a), "layernorm_param_sums: missing inputs");
-  if (hz::active()) {
-    using namespace hz;
-    const int64_t row = a.d * (int64_t)dsize(t), sb = a.d * 4, ss = std::max<int64_t>(a.stripe_stride * 4, sb);
-    op(s, "ln_param_sums", {rd(a.dy, a.M * row), rd(a.v, a.M * row), rd(a.mean, a.M * 4), rd(a.rstd, a.M * 4),
-                            rd(a.d_a, a.M * row), blk(a.dgamma, a.stripes, sb, ss, ACC), blk(a.dbeta, a.stripes, sb, ss, ACC),
-                            blk(a.dbias, a.stripes, sb, ss, ACC)});
-  }
-  if (t == DType::F32) ln_sums_dispatch<float>(a, s);
-  else ln_sums_dispatch<bf16>(a, s);
-  CAPGEN_HIP(hipGetLastError());
 }
 
 template <typename T>
@@ -332,56 +251,29 @@ void layernorm_fwd(const LnFwd& a_in, DType t, hipStream_t s) {
   CAPGEN_HIP(hipGetLastError());
 }
 
-template <typename T, int R, int NT = LN_THREADS>
-static void ln_bwd_dispatch_r(const LnBwd& a, hipStream_t s) {
-  // R rows per wave (one loop trip at C2 for R = 2), <= 512 workgroups: few enough dgamma/dbeta atomics
-  constexpr int W = NT / 64;
-  dim3 grid(std::min(512, (a.M + W * R - 1) / (W * R)));
-  switch (a.d / 64) {
-    case 1: ln_bwd_kernel<T, 1, R, NT><<<grid, NT, 0, s>>>(a); break;
-    case 2: ln_bwd_kernel<T, 2, R, NT><<<grid, NT, 0, s>>>(a); break;
-    case 4: ln_bwd_kernel<T, 4, R, NT><<<grid, NT, 0, s>>>(a); break;
-    case 8: ln_bwd_kernel<T, 8, R, NT><<<grid, NT, 0, s>>>(a); break;
-    case 16: ln_bwd_kernel<T, 16, R, NT><<<grid, NT, 0, s>>>(a); break;
-    default: throw Error("layernorm: width must be 64 * {1,2,4,8,16}");
-  }
-}
 template <typename T>
 static void ln_bwd_dispatch(const LnBwd& a, hipStream_t s) {
-  // rows per wave (CAPGEN_LNB_ROWS: 1, 2 or 4).  Default 1: with 2 rows per wave the two-engine
-  // bf16 probe diverged in 12-14 of 30 comparisons with 2 streams, always first in a row this
-  // kernel computes last in its wave, with every input of the kernel equal;
-  // with 1 row per wave, 0 of 30.
-  static const int rows = [] {
-    const char* e = std::getenv("CAPGEN_LNB_ROWS");
-    return e ? std::atoi(e) : 1;
-  }();
-  static const int waves = [] {  // experiment knob: waves per workgroup (4 or 8)
-    const char* e = std::getenv("CAPGEN_LNB_WAVES");
-    return e ? std::atoi(e) : 4;
-  }();
-  if (waves == 8) ln_bwd_dispatch_r<T, 2, 512>(a, s);
-  else if (rows == 1) ln_bwd_dispatch_r<T, 1>(a, s);
-  else if (rows == 4) ln_bwd_dispatch_r<T, 4>(a, s);
-  else ln_bwd_dispatch_r<T, 2>(a, s);
+  constexpr int W = LN_THREADS / 64;  // one row per wave, no loop
+  dim3 grid((a.M + W - 1) / W);
+  switch (a.d / 64) {
+    case 1: ln_bwd_kernel<T, 1><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 2: ln_bwd_kernel<T, 2><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 4: ln_bwd_kernel<T, 4><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 8: ln_bwd_kernel<T, 8><<<grid, LN_THREADS, 0, s>>>(a); break;
+    case 16: ln_bwd_kernel<T, 16><<<grid, LN_THREADS, 0, s>>>(a); break;
+    default: throw Error("layernorm: width must be 64 * {1,2,4,8,16}");
+  }
 }
 void layernorm_bwd(const LnBwd& a_in, DType t, hipStream_t s) {
   if (a_in.M <= 0 || (skip_mask() & 4)) return;
   LnBwd a = a_in;
   if (a.wt < 0) a.wt = wt_default();
-  if (a.coh < 0) {
-    static const int coh = [] {
-      const char* e = std::getenv("CAPGEN_LNB_COH");
-      return e ? std::atoi(e) : 0;
-    }();
-    a.coh = coh;
-  }
   if (hz::active()) {
     using namespace hz;
     const int64_t row = a.d * (int64_t)dsize(t), sb = a.d * 4, ss = std::max<int64_t>(a.stripe_stride * 4, sb);
     op(s, "ln_bwd", {rd(a.dy, a.M * row), rd(a.v, a.M * row), rd(a.mean, a.M * 4), rd(a.rstd, a.M * 4),
                      rd(a.gamma, a.d * 4), blk(a.mask.ids, a.M, 4, a.mask.ids_ld * 4, RD), rd(a.mask.valid, a.M),
-                     rd(a.drop.seed_ptr, 8), wr(a.d_res, a.M * row), wr(a.d_a, a.M * row), wr(a.y_save, a.M * row),
+                     rd(a.drop.seed_ptr, 8), wr(a.d_res, a.M * row), wr(a.d_a, a.M * row),
                      blk(a.dgamma, a.stripes, sb, ss, ACC), blk(a.dbeta, a.stripes, sb, ss, ACC),
                      blk(a.dbias, a.stripes, sb, ss, ACC)});
   }

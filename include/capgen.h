@@ -165,9 +165,10 @@ int capgen_debug_splitk_diag(int* out4, int reset);
 /* Diagnostic (GEMM ablation build only, protocol bit 4096): device buffer (>= 88 u64) that block 0 of
  * the next GEMM launches fills with per-phase s_memtime / s_memrealtime stamps (gemm_bf16.hip ABL_T). */
 int capgen_debug_gemm_timing_buf(void* dev_buf);
-/* Diagnostic: synchronous copy of an internal gradient buffer (0 tmp, 1 gOut, 2 gRes, 3 cross-K/V
- * gradient, 4-7 the last encoder block's FFN-hidden / FFN-LN / MHA-LN / QKV gradients) to host;
- * with CAPGEN_DEBUG_BWD_STOP the backward pass ends early (tools/bwd_bisect.py). */
+/* Diagnostic: synchronous copy of an internal buffer to host: 0 tmp, 1 gOut, 2 gRes, 3 cross-K/V
+ * gradient, 4-7 the last encoder block's FFN-hidden / FFN-LN / MHA-LN / QKV gradients; 32 + 8 l + j
+ * encoder block l's gAf / gH / gA1 / gATT1 / gQKV; 80 + l the encoder activations X[l]; 128 + 8 l + j
+ * encoder block l's saved forward tensors (att, v1, m1, r1, Y, v2, m2, r2). */
 int capgen_debug_copy_buffer(capgen_t* h, int which, void* host_dst, int64_t bytes);
 
 /* Training step over an HBM-resident feature store (replaces TrainDataset.__getitem__ + the

@@ -145,10 +145,12 @@ RL_WEIGHTS = dict(structure_loss_weight=0.5, cider_reward_weight=1.0, bleu_rewar
                   entropy_reward_weight=1.0, self_cider_reward_weight=1.0)
 
 
-def make_rl_fixture(tag, cfg, B, N, T, seed, min_valid=None, pad_frac=0.0):
+def make_rl_fixture(tag, cfg, B, N, T, seed, min_valid=None, pad_frac=0.0, store_inputs=True):
     """pad_frac > 0: raise the classifier bias of the pad id so that about that fraction of the
     argmax samples are 0 (exercises the structure-loss mask; the boost is stored as
-    `pad_bias_boost` and applied to the fixture weights by the tests)."""
+    `pad_bias_boost` and applied to the fixture weights by the tests).  store_inputs=False (the
+    full C5 shape): the batch is not stored -- the tests regenerate it with
+    capgen.synthetic.synthetic_batch from the recorded (B, N, T, V, seed, min_valid)."""
     import pickle
     import tempfile
     import_reference()
@@ -219,8 +221,12 @@ def make_rl_fixture(tag, cfg, B, N, T, seed, min_valid=None, pad_frac=0.0):
     crit = ReinforcementLearningLoss(word_to_idx_path=vocab_path, pad_idx=cfg.pad_idx, **RL_WEIGHTS)
     os.unlink(vocab_path)
 
-    out = {"feats": feats.numpy(), "pos": pos.numpy(), "caps": caps.numpy(),
-           "inj_cider": cider, "inj_bleu": bleu, "pad_bias_boost": np.float64(boost)}
+    out = {"inj_cider": cider, "inj_bleu": bleu, "pad_bias_boost": np.float64(boost)}
+    if store_inputs:
+        out.update(feats=feats.numpy(), pos=pos.numpy(), caps=caps.numpy())
+    else:
+        out.update(batch_shape=np.array([B, N, T, cfg.num_vocab]), batch_seed=np.int64(seed + 100),
+                   batch_min_valid=np.int64(-1 if min_valid is None else min_valid))
     for k, v in RL_WEIGHTS.items():
         out[k] = np.float64(v)
     logits = model(object_features=feats, position_features=pos, target_caption=caps)
@@ -310,6 +316,10 @@ RL_FIXTURES = {
     # the C5 model itself (6+6 blocks, d=512, h=8, 36 regions, T=20) at the c2s vocabulary
     "c5_rl_c2s": (preset("C2", num_vocab=1000), 4, 36, 20, 12, 12, 0.2),
 }
+# C5's own shape (SCST on the C2 model, 64 images per GPU, V=10000); inputs regenerated
+RL_FIXTURES_SEEDED = {
+    "c5_rl_c5": (preset("C2"), 64, 36, 20, 13, None, 0.2),
+}
 
 
 FIXTURES = {
@@ -338,6 +348,10 @@ def main(tags=None):
         if tags and tag not in tags:
             continue
         make_rl_fixture(tag, cfg, B, N, T, seed, min_valid=mv, pad_frac=pf)
+    for tag, (cfg, B, N, T, seed, mv, pf) in RL_FIXTURES_SEEDED.items():
+        if tags and tag not in tags:
+            continue
+        make_rl_fixture(tag, cfg, B, N, T, seed, min_valid=mv, pad_frac=pf, store_inputs=False)
 
 
 if __name__ == "__main__":

@@ -40,9 +40,6 @@ MODES = {
     "serial_dec0": {"CAPGEN_OVERLAP_DEC0": "0"},
     "front_after_encoder": {"CAPGEN_OVERLAP_FRONT": "0"},
     "single_dw_launches": {"CAPGEN_GROUP_DW": "0"},
-    "split_enc_grad": {"CAPGEN_SPLIT_ENC_GRAD": "1"},
-    "kv_split": {"CAPGEN_KV_SPLIT": "1"},
-    "ln_sums_side": {"CAPGEN_LN_SUMS_SIDE": "1"},
     "colsum_in_epilogue": {"CAPGEN_COLSUM_SIDE": "0"},
     "two_blocks_per_bucket": {"CAPGEN_BUCKET_BLOCKS": "2"},
     "stripe_memset": {"CAPGEN_STRIPE_CLEAR": "0"},

@@ -5,7 +5,7 @@ import pytest
 import torch
 
 from capgen.params import fixture_state_dict, reference_param_specs, sinusoid_table
-from golden_util import load_fixture, sample_index
+from golden_util import fixture_inputs, load_fixture, sample_index
 from oracle import capgen_oracle as O
 
 TAGS = ["c1", "c1_encmask", "c1_focal", "c2s", "c1_splitpos", "c1_imgobj", "c1_movefirst"]
@@ -99,12 +99,12 @@ def rl_setup(tag):
     sd = fixture_state_dict(cfg, seed=seed, with_buffer=False)
     sd["classifer.bias"] = sd["classifer.bias"].copy()
     sd["classifer.bias"][0] += float(z["pad_bias_boost"])
-    x = [torch.from_numpy(z[k]) for k in ("feats", "pos", "caps")]
+    x = fixture_inputs(z)
     base = float(z["cider_reward_weight"]) * z["inj_cider"] + float(z["bleu_reward_weight"]) * z["inj_bleu"]
     return cfg, sd, x, z, base
 
 
-@pytest.mark.parametrize("tag", ["c5_rl", "c5_rl_pad", "c5_rl_c2s"])
+@pytest.mark.parametrize("tag", ["c5_rl", "c5_rl_pad", "c5_rl_c2s", "c5_rl_c5"])
 def test_rl_loss_and_grads(tag):
     """SelfCriticNetwork step mechanics (model_RL.py:75-97, loss.py:31-220) with injected rewards."""
     cfg, sd, (f, p, c), z, base = rl_setup(tag)

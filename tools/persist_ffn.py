@@ -13,6 +13,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "image-caption_amd"))
+os.environ.setdefault("CAPGEN_PERSIST_OK", "1")  # the experiment hook is opt-in
 import torch  # noqa: E402
 
 from capgen import _lib  # noqa: E402
