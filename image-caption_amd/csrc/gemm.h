@@ -28,7 +28,7 @@ struct GemmArgs {
   const float* alpha_ptr = nullptr;  // device scalar multiplied into alpha (e.g. 1/count)
   int beta = 0;                      // 1: accumulate into C
   int prio = 0;                      // 1: critical-path launch, waves raise their issue priority
-  const float* cin = nullptr;        // += cin[m][n] (f32, row stride ldcin) before the activation
+  const float* cin = nullptr;        // unsupported (must stay null; kept so the argument layout is unchanged)
   int64_t ldcin = 0;
   void* C2 = nullptr;                // bf16 path: columns n >= nsplit go to C2[m][n - nsplit] (row
   int64_t ldc2 = 0;                  //   stride ldc2), e.g. Q to one buffer and K/V to a cache

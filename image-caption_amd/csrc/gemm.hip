@@ -287,7 +287,7 @@ static void gemm_impl(const GemmArgs& g, DType in, DType out, bool ta, bool tb, 
   require(((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0, "gemm: operands must be 16-B aligned");
   require(g.K > 0, "gemm: K must be positive");
   require(!g.colsum || !g.beta, "gemm: colsum requires beta == 0");
-  require(!g.cin || in == DType::BF16, "gemm: cin is a bf16-path epilogue input");
+  require(!g.cin, "gemm: the cin epilogue input is not supported (removed with its only user)");
   require(!g.dec_stats || in == DType::BF16, "gemm: dec_stats is a bf16-path epilogue output");
   require(!g.C2 || (in == DType::BF16 && g.nsplit % 4 == 0 && !g.beta && !g.colsum),
           "gemm: a split output (C2) needs the bf16 path, nsplit % 4 == 0, no beta / colsum");

@@ -449,24 +449,41 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int mt, int nt, int
     if (!*flag) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the ticket
     const int lpol = (proto & 256) ? 17 : (proto & 4) ? 16 /* sc1 */ : 0;
+    // slice by slice in slice order (deterministic, and the k-group exchange's order: 0 + p0 + p1 + ...);
+    // every fragment's load of one slice is issued before any is used (one round trip per slice, not
+    // per slice and fragment)
+    f32x4 sum[FM][FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int sl = 0; sl < splitk; ++sl) {
-          if (sl == split) {
-            sum += acc[i][j];
-          } else {
-            const int off = ((sl * NF + i * FN + j) * NT + tid) * 16;
-            const u32x4 o = lpol == 17 ? __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 17)
-                            : lpol     ? __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 16)
-                                       : __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
-            sum += __builtin_bit_cast(f32x4, o);
-          }
-        }
-        acc[i][j] = sum;
+      for (int j = 0; j < FN; ++j) sum[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int sl = 0; sl < splitk; ++sl) {
+      if (sl == split) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) sum[i][j] += acc[i][j];
+        continue;
       }
+      u32x4 o[FM][FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int off = ((sl * NF + i * FN + j) * NT + tid) * 16;
+          o[i][j] = lpol == 17 ? __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 17)
+                    : lpol     ? __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 16)
+                               : __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
+        }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) sum[i][j] += __builtin_bit_cast(f32x4, o[i][j]);
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = sum[i][j];
   }
   tile_epilogue<TO, FM, FN, TM, TN>(g, acc, m0, n0, wm, wn, lane, alpha);
   ABL_T(35);
@@ -487,11 +504,21 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&a
       // a 16x16 fragment = 16 rows x one 16-column slab; the 4 lanes of a row (lane groups fq)
       // hold its 4 column quads, so slab max / sum are two xor-shuffles.  Every lane runs the
       // shuffles (partners share the row, so out-of-range rows only predicate the stores).
+      // every bias / target load first (clamped addresses, unconditional): one round trip
+      float4 bq[FN];
+      int tgq[FM];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = min(n0 + wn * TN + j * 16 + fq * 4, g.N - 4);
+        bq[j] = g.bias ? *reinterpret_cast<const float4*>(g.bias + n) : float4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i) tgq[i] = g.ce_tgt[min(m0 + wm * TM + i * 16 + fr, g.M - 1)];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int m = m0 + wm * TM + i * 16 + fr;
         const bool mok = m < g.M;
-        const int tg = mok ? g.ce_tgt[m] : -1;
+        const int tg = mok ? tgq[i] : -1;
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           if ((i * FN + j) % kgs != kgrp) continue;  // (k-groups: another group stores it)
@@ -499,7 +526,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&a
           const bool nok = n < g.N;
           float v[4], mx = -INFINITY;
           if (nok) {
-            const float4 b4 = g.bias ? *reinterpret_cast<const float4*>(g.bias + n) : float4{0.f, 0.f, 0.f, 0.f};
+            const float4 b4 = bq[j];
             v[0] = alpha * acc[i][j][0] + b4.x, v[1] = alpha * acc[i][j][1] + b4.y;
             v[2] = alpha * acc[i][j][2] + b4.z, v[3] = alpha * acc[i][j][3] + b4.w;
             mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
@@ -528,6 +555,12 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&a
     if (g.dec_stats) {  // decode classifier epilogue (GemmArgs::dec_stats): f32 logits + slab stats
       // same fragment geometry as the cross-entropy epilogue above: the 4 lane groups of a row hold
       // its 16-column slab, so the slab max / exp-sum are two xor-shuffles
+      float4 bq[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = min(n0 + wn * TN + j * 16 + fq * 4, g.N - 4);
+        bq[j] = g.bias ? *reinterpret_cast<const float4*>(g.bias + n) : float4{0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int m = m0 + wm * TM + i * 16 + fr;
@@ -539,7 +572,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&a
           const bool nok = n < g.N;
           float v[4], mx = -INFINITY;
           if (nok) {
-            const float4 b4 = g.bias ? *reinterpret_cast<const float4*>(g.bias + n) : float4{0.f, 0.f, 0.f, 0.f};
+            const float4 b4 = bq[j];
             v[0] = alpha * acc[i][j][0] + b4.x, v[1] = alpha * acc[i][j][1] + b4.y;
             v[2] = alpha * acc[i][j][2] + b4.z, v[3] = alpha * acc[i][j][3] + b4.w;
             mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
@@ -558,33 +591,67 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&a
       return;
     }
   }
+  // Generic epilogue.  Every side-operand load of the tile (bias, ReLU' mask, the accumulated C) is
+  // issued before the first store: the loads of one fragment used to wait for the previous fragment's
+  // store (hipcc cannot move a load across a store in another basic block), one memory round trip per
+  // fragment and operand -- the ReLU'-masked FFN input-gradient GEMMs ran at 2.5x their forward twins
+  // in the step.  (The f32 cin operand of the removed split-encoder-gradient experiment is gone.)
+  typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+  float bn[FN][4];
+  u32x2 auxr[FM][FN];          // 4 bf16 of the ReLU' mask
+  float cold[FM][FN][4];       // beta: the C values accumulated into
+  bool ok[FM][FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wn * TN + j * 16 + fq * 4;
+    const bool nok = n < g.N;
+    float4 b4 = float4{0.f, 0.f, 0.f, 0.f};
+    if (g.bias && nok) b4 = *reinterpret_cast<const float4*>(g.bias + n);
+    bn[j][0] = b4.x, bn[j][1] = b4.y, bn[j][2] = b4.z, bn[j][3] = b4.w;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = m0 + wm * TM + i * 16 + fr;
+      ok[i][j] = nok && m < g.M && (i * FN + j) % kgs == kgrp;
+    }
+  }
+  if (aux) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int m = min(m0 + wm * TM + i * 16 + fr, g.M - 1), n = min(n0 + wn * TN + j * 16 + fq * 4, g.N - 4);
+        auxr[i][j] = *reinterpret_cast<const u32x2*>(aux + (int64_t)m * g.ldaux + n);
+      }
+  }
+  if (g.beta) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        // (clamped in-range address, loaded unconditionally: a load inside a per-fragment branch is
+        // waited for at the branch's join)
+        const int m = min(m0 + wm * TM + i * 16 + fr, g.M - 1), n = min(n0 + wn * TN + j * 16 + fq * 4, g.N - 4);
+        const bool hi = C2 && n >= g.nsplit;
+        const TO* cp = hi ? C2 + (int64_t)m * g.ldc2 + (n - g.nsplit) : C + (int64_t)m * g.ldc + n;
+        load4<TO>(cp, cold[i][j]);
+      }
+  }
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int n = n0 + wn * TN + j * 16 + fq * 4;
     float cs[4] = {0.f, 0.f, 0.f, 0.f};
     if (n >= g.N) continue;
     const bool hi = C2 && n >= g.nsplit;  // split output: this 4-column group goes to C2
-    float bn[4] = {0.f, 0.f, 0.f, 0.f};
-    if (g.bias) {
-      float4 b4 = *reinterpret_cast<const float4*>(g.bias + n);
-      bn[0] = b4.x, bn[1] = b4.y, bn[2] = b4.z, bn[3] = b4.w;
-    }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int m = m0 + wm * TM + i * 16 + fr;
-      if (m >= g.M || (i * FN + j) % kgs != kgrp) continue;
+      if (!ok[i][j]) continue;
       float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = alpha * acc[i][j][r] + bn[r];
-      if (g.cin) {
-        float c4[4];
-        load4<float>(g.cin + (int64_t)m * g.ldcin + n, c4);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += c4[r];
-      }
+      for (int r = 0; r < 4; ++r) v[r] = alpha * acc[i][j][r] + bn[j][r];
       if (aux) {
-        float a4[4];
-        load4<bf16>(aux + (int64_t)m * g.ldaux + n, a4);
+        const float a4[4] = {__uint_as_float(auxr[i][j][0] << 16), __uint_as_float(auxr[i][j][0] & 0xffff0000u),
+                             __uint_as_float(auxr[i][j][1] << 16), __uint_as_float(auxr[i][j][1] & 0xffff0000u)};
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = a4[r] > 0.f ? v[r] : 0.f;
       }
@@ -594,10 +661,8 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, const f32x4 (&a
       }
       TO* cp = hi ? C2 + (int64_t)m * g.ldc2 + (n - g.nsplit) : C + (int64_t)m * g.ldc + n;
       if (g.beta) {
-        float o[4];
-        load4<TO>(cp, o);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += o[r];
+        for (int r = 0; r < 4; ++r) v[r] += cold[i][j][r];
       }
       if (g.wt > 0 && !hi) {  // write-through (capgen_common.h wt_rsrc)
         const uint32_t off = (uint32_t)(((int64_t)m * g.ldc + n) * (int64_t)sizeof(TO));
