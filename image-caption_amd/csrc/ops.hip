@@ -25,6 +25,22 @@ constexpr int LN_THREADS = 256;  // 4 rows per workgroup
 constexpr float LN_EPS = 1e-6f;  // modules.py:57,105
 
 
+// target of the LayerNorm kernels' absent optional inputs (zeros: residual, bias, positional row)
+struct LnDummy {
+  float zero[1024];  // the widest row (d = 64 * 16)
+  uint64_t seed;
+  int32_t id;
+  uint8_t valid;
+};
+__device__ LnDummy g_ln_dummy = {{}, 0, 0, 1};
+// a wave-uniform pointer the compiler must treat as an unknown SGPR value
+template <typename P>
+__device__ __forceinline__ P* opaque(P* p) {
+  uint64_t v = reinterpret_cast<uint64_t>(p);
+  asm volatile("" : "+s"(v));
+  return reinterpret_cast<P*>(v);
+}
+
 // Every global load of the row (input, residual, bias, positional row, gamma, beta, row mask,
 // dropout seed) is issued before the first store: the kernel pays ONE memory round trip (the
 // stores could alias the parameter pointers, so the compiler would not hoist them itself).
@@ -42,14 +58,28 @@ __global__ void __launch_bounds__(LN_THREADS) ln_fwd_kernel(LnFwd a) {
   const int d = a.d, c0 = lane * DPL;
   const int64_t base = (int64_t)m * d + c0;
   float x[DPL], r[DPL], bias[DPL], pe[DPL], gm[DPL], bt[DPL];
+  // optional inputs through a pointer select (absent -> a device dummy of zeros), loaded
+  // unconditionally: a load inside a branch is waited for at the branch's join (one more round
+  // trip per optional input; the ISA of the branchy form had five)
+  // (the uniform base pointers go through opaque() so hipcc cannot turn the select back into a branch)
+  const T* res_p = opaque(a.res ? reinterpret_cast<const T*>(a.res) : reinterpret_cast<const T*>(g_ln_dummy.zero)) +
+                   (a.res ? base : c0);
+  const float* bias_p = opaque(a.a_bias ? a.a_bias : g_ln_dummy.zero) + c0;
+  const float* pe_p = opaque(a.pe ? a.pe : g_ln_dummy.zero) + (a.pe ? (int64_t)(m % max(a.pe_L, 1)) * d : 0) + c0;
+  const uint64_t* seed_p = opaque(a.drop.seed_ptr ? a.drop.seed_ptr : &g_ln_dummy.seed);
+  const int32_t* ids_p = opaque(a.mask.ids ? a.mask.ids : &g_ln_dummy.id) + (a.mask.ids ? (int64_t)m * a.mask.ids_ld : 0);
+  const uint8_t* val_p = opaque(a.mask.valid ? a.mask.valid : &g_ln_dummy.valid) + (a.mask.valid ? m : 0);
+  const uint64_t seed_v = *seed_p;
+  const int idv = *ids_p;
+  const int vld = *val_p;
   load_f<T, DPL>(reinterpret_cast<const T*>(a.a) + base, x);
-  if (a.res) load_f<T, DPL>(reinterpret_cast<const T*>(a.res) + base, r);
-  if (a.a_bias) load_f32<DPL>(a.a_bias + c0, bias);
-  if (a.pe) load_f32<DPL>(a.pe + (int64_t)(m % a.pe_L) * d + c0, pe);
+  load_f<T, DPL>(res_p, r);
+  load_f32<DPL>(bias_p, bias);
+  load_f32<DPL>(pe_p, pe);
   load_f32<DPL>(a.gamma + c0, gm);
   load_f32<DPL>(a.beta + c0, bt);
-  const bool kept = row_kept(a.mask, m);
-  const uint64_t seed = a.drop.seed_ptr ? *a.drop.seed_ptr : 0;
+  const bool kept = !(a.mask.ids && idv == a.mask.pad_idx) && !(a.mask.valid && vld == 0);
+  const uint64_t seed = a.drop.seed_ptr ? seed_v : 0;
   if (a.a_bias) {
 #pragma unroll
     for (int e = 0; e < DPL; ++e) x[e] += bias[e];
@@ -102,13 +132,6 @@ __global__ void __launch_bounds__(LN_THREADS) ln_fwd_kernel(LnFwd a) {
   }
 }
 
-struct LnDummy {
-  uint64_t seed;
-  int32_t id;
-  uint8_t valid;
-};
-__device__ LnDummy g_ln_dummy = {0, 0, 1};
-
 // One row per wave.  The row index is wave-uniform (readfirstlane), so the row statistics, the row
 // mask and the dropout seed are scalar loads, issued together with the row's two 16-B vector loads
 // (dy, v) and gamma before any use: one memory round trip per row.
@@ -135,9 +158,10 @@ __global__ void __launch_bounds__(NT) ln_bwd_kernel(LnBwd a) {
   int idv = 0, vld = 1;
   // optional inputs are read through a pointer select (absent -> a device dummy), never inside a
   // branch: a load in a branch makes hipcc wait for it at the join, one more round trip each
-  const uint64_t* seed_p = a.drop.seed_ptr ? a.drop.seed_ptr : &g_ln_dummy.seed;
-  const int32_t* ids_p = a.mask.ids ? a.mask.ids + (int64_t)min(m, a.M - 1) * a.mask.ids_ld : &g_ln_dummy.id;
-  const uint8_t* val_p = a.mask.valid ? a.mask.valid + min(m, a.M - 1) : &g_ln_dummy.valid;
+  const uint64_t* seed_p = opaque(a.drop.seed_ptr ? a.drop.seed_ptr : &g_ln_dummy.seed);
+  const int32_t* ids_p = opaque(a.mask.ids ? a.mask.ids : &g_ln_dummy.id) +
+                         (a.mask.ids ? (int64_t)min(m, a.M - 1) * a.mask.ids_ld : 0);
+  const uint8_t* val_p = opaque(a.mask.valid ? a.mask.valid : &g_ln_dummy.valid) + (a.mask.valid ? min(m, a.M - 1) : 0);
   const uint64_t seed_v = *seed_p;
   const int idv_v = *ids_p;
   const int vld_v = *val_p;

@@ -46,15 +46,25 @@ def main():
         s = torch.cuda.Stream(dev)
         refH = torch.relu(X.float() @ W1.float().t() + b1)
         for grid in (1, 2, 8, 64):
+            H.fill_(float("nan"))
+            Y.fill_(float("nan"))
             t0 = time.perf_counter()
             _lib.check(lib.capgen_debug_ffn_persist(M, d, fe, ptr(X), ptr(W1), ptr(b1), ptr(W2), ptr(H), ptr(Y), grid, 1,
                                                     C.c_void_p(s.cuda_stream)))
             torch.cuda.synchronize()
             gv = C.c_int(0)
             _lib.check(lib.capgen_debug_persist_giveups(1, C.byref(gv)))
+            refY = H.float() @ W2.float().t()
+            # per 64-column W2 tile: never written (NaN left), wrong, or right
+            tiles = []
+            for nt in range(d // 64):
+                yt, rt = Y[:, nt * 64:(nt + 1) * 64].float(), refY[:, nt * 64:(nt + 1) * 64]
+                tiles.append("nan" if torch.isnan(yt).any() else
+                             ("ok" if (yt - rt).abs().max() <= 0.05 * rt.abs().max() else "bad"))
             print(json.dumps({"grid": grid, "ms": round((time.perf_counter() - t0) * 1e3, 2), "giveups": gv.value,
                               "H_maxerr": float((H.float() - refH).abs().max()),
-                              "Y_maxerr": float((Y.float() - H.float() @ W2.float().t()).abs().max())}), flush=True)
+                              "Y_maxerr": float((Y.float() - refY).abs().nan_to_num(1e30).max()),
+                              "Y_tiles": tiles}), flush=True)
         return
     for name, M, d, fe in (("enc FFN", 2304, 512, 2048), ("dec FFN", 1216, 512, 2048)):
         X = (torch.randn(M, d, device=dev) * 0.5).to(torch.bfloat16)
