@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CAPGEN_LIB_PATH") or os.path.join(_HERE, "libcapgen.so")  # (diagnostic builds)
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 F32, BF16 = 0, 1
 
@@ -71,8 +71,6 @@ _SIGS = {
     "capgen_debug_gemm": (C.c_int, [C.c_int, C.c_int, C.c_int, _P, C.c_int64, C.c_int, _P, C.c_int64, C.c_int,
                                     _P, C.c_int64, C.c_int, C.c_int, _P, C.c_float, C.c_int, C.c_int, _P]),
     "capgen_debug_gemm_variant": (C.c_int, [C.c_int]),
-    "capgen_debug_ffn_persist": (C.c_int, [C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, C.c_int, C.c_int, _P]),
-    "capgen_debug_persist_giveups": (C.c_int, [C.c_int, _P]),
     "capgen_debug_splitk_protocol": (C.c_int, [C.c_int]),
     "capgen_debug_splitk_diag": (C.c_int, [_P, C.c_int]),
     "capgen_debug_gemm_timing_buf": (C.c_int, [_P]),
@@ -83,6 +81,7 @@ _SIGS = {
     "capgen_rl_finish": (C.c_int, [_P, _P, C.c_float, _P, C.c_int, _P]),
     "capgen_debug_attention": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P,
                                          C.c_int, C.c_float, _P, _P, _P, _P, _P, _P, _P]),
+    "capgen_debug_qkv_attention": (C.c_int, [C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, C.c_int, C.c_int, _P]),
     "capgen_dp_unique_id": (C.c_int, [C.c_char_p]),
     "capgen_dp_init": (C.c_int, [_P, C.c_char_p, C.c_int, C.c_int]),
     "capgen_dp_set_global_count": (C.c_int, [_P, C.c_float]),

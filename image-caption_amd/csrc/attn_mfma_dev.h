@@ -1,6 +1,6 @@
 // capgen — bf16 MFMA attention building blocks (helpers + the forward of one (batch, head)) as
-// device code shared by the attention launches (attention_mfma.hip) and the persistent
-// encoder-layer kernel (persist.hip).  Design notes: attention_mfma.hip header.
+// device code shared by the attention launches (attention_mfma.hip) and the fused Q/K/V projection +
+// attention kernel (qkv_attn.hip).  Design notes: attention_mfma.hip header.
 #pragma once
 #include "attention.h"
 
@@ -128,26 +128,15 @@ __device__ __forceinline__ void store4(bf16* p, f32x4 v, float mul) {
 }
 
 
-// forward of one (batch b, head h): 256 threads, sm = 3 [64][64] bf16 images + 64 key flags
-__device__ __forceinline__ void attn_fwd_one(const AttnGeom& g, bf16* __restrict__ o, float* __restrict__ probs, int b,
-                                             int h, char* sm) {
-  char* Qimg = sm;
-  char* Kimg = sm + IMG;
-  char* Vimg = sm + 2 * IMG;
-  unsigned char* kok = reinterpret_cast<unsigned char*>(sm + 3 * IMG);
+// forward of one (batch b, head h) once Q / K / V sit in the LDS images sm[0..3) and the key flags
+// after them (zero rows beyond Lq / Lk): S = Q K^T -> mask -> softmax -> [probs] -> dropout -> O = P V
+__device__ __forceinline__ void attn_fwd_staged(const AttnGeom& g, bf16* __restrict__ o, float* __restrict__ probs,
+                                                int b, int h, const char* sm) {
+  const char* Qimg = sm;
+  const char* Kimg = sm + IMG;
+  const char* Vimg = sm + 2 * IMG;
+  const unsigned char* kok = reinterpret_cast<const unsigned char*>(sm + 3 * IMG);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int bk = g.kv_bmod ? b % g.kv_bmod : b;
-  {
-    char* const img[3] = {Qimg, Kimg, Vimg};
-    const bf16* const src[3] = {reinterpret_cast<const bf16*>(g.q) + (int64_t)b * g.q_bs + h * DK,
-                                reinterpret_cast<const bf16*>(g.k) + (int64_t)bk * g.k_bs + h * DK,
-                                reinterpret_cast<const bf16*>(g.v) + (int64_t)bk * g.v_bs + h * DK};
-    const int64_t ld[3] = {g.q_ld, g.k_ld, g.v_ld};
-    const int L[3] = {g.Lq, g.Lk, g.Lk};
-    stage_images<3>(img, src, ld, L, tid);
-    stage_key_ok(kok, g, b, tid);
-  }
-  __syncthreads();
   const int q0 = 16 * w, q = q0 + (lane & 15);
   if (q0 >= g.Lq) return;
   f32x4 s[4], p[4];
@@ -184,6 +173,29 @@ __device__ __forceinline__ void attn_fwd_one(const AttnGeom& g, bf16* __restrict
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_t(Vimg, 16 * t, 1, lane), pf1, acc, 0, 0, 0);
     if (q < g.Lq) store4(ob + (int64_t)q * g.o_ld + 16 * t + 4 * (lane >> 4), acc, 1.f);
   }
+}
+
+// forward of one (batch b, head h): 256 threads, sm = 3 [64][64] bf16 images + 64 key flags
+__device__ __forceinline__ void attn_fwd_one(const AttnGeom& g, bf16* __restrict__ o, float* __restrict__ probs, int b,
+                                             int h, char* sm) {
+  char* Qimg = sm;
+  char* Kimg = sm + IMG;
+  char* Vimg = sm + 2 * IMG;
+  unsigned char* kok = reinterpret_cast<unsigned char*>(sm + 3 * IMG);
+  const int tid = threadIdx.x;
+  const int bk = g.kv_bmod ? b % g.kv_bmod : b;
+  {
+    char* const img[3] = {Qimg, Kimg, Vimg};
+    const bf16* const src[3] = {reinterpret_cast<const bf16*>(g.q) + (int64_t)b * g.q_bs + h * DK,
+                                reinterpret_cast<const bf16*>(g.k) + (int64_t)bk * g.k_bs + h * DK,
+                                reinterpret_cast<const bf16*>(g.v) + (int64_t)bk * g.v_bs + h * DK};
+    const int64_t ld[3] = {g.q_ld, g.k_ld, g.v_ld};
+    const int L[3] = {g.Lq, g.Lk, g.Lk};
+    stage_images<3>(img, src, ld, L, tid);
+    stage_key_ok(kok, g, b, tid);
+  }
+  __syncthreads();
+  attn_fwd_staged(g, o, probs, b, h, sm);
 }
 
 constexpr int kFwdSmem = 3 * IMG + 64;

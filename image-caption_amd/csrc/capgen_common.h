@@ -143,6 +143,16 @@ __device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, uint32_t off,
   }
 }
 
+// A wave-uniform pointer the compiler must treat as an unknown SGPR value: a select between an
+// optional input and a device dummy stays a select (hipcc otherwise turns it back into a branch
+// around the load, and waits for the load at the branch's join -- one memory round trip each).
+template <typename P>
+__device__ __forceinline__ P* opaque(P* p) {
+  uint64_t v = reinterpret_cast<uint64_t>(p);
+  asm volatile("" : "+s"(v));
+  return reinterpret_cast<P*>(v);
+}
+
 // ---- wave64 reductions ----------------------------------------------------------------
 // Lane exchanges inside a 16-lane row are DPP moves (a VALU operand modifier, no LDS crossbar):
 // quad_perm swaps lanes ^1 and ^2, row_half_mirror pairs lane i with 7 - i (the other quad of the

@@ -27,8 +27,8 @@
 #include "gemm.h"
 #include "hazard.h"
 #include "layout.h"
-#include "persist.h"
 #include "ops.h"
+#include "qkv_attn.h"
 #include "variants.h"
 #include "rl.h"
 
@@ -388,6 +388,32 @@ struct capgen_engine {
     attention_bwd(g, probs, dout, dq, dk, dv, t, s);
   }
 
+  // The self-attention front of a block (modules.py:67-76 + 16-27): qkv = X . Wqkv^T, then the
+  // attention of g over it into att.  bf16 with head size 64 and d = 512: ONE fused launch
+  // (qkv_attn.hip: projection straight into the attention's LDS images; qkv still written for the
+  // backward).  Otherwise (f32 parity mode, other geometries, CAPGEN_FUSED_QKV=0) the GEMM and the
+  // attention launch.
+  bool fused_qkv_on = [] {
+    const char* e = std::getenv("CAPGEN_FUSED_QKV");
+    return !(e && e[0] == '0');
+  }();
+  void self_attention(const void* X, int64_t wqkv, int M, int d, const AttnGeom& g, void* qkv, void* att, float* probs,
+                      hipStream_t s) {
+    if (fused_qkv_on && act == DType::BF16 && !keep_probs(g)) {
+      QkvAttn qa;
+      qa.g = g, qa.g.prio = prio(s);
+      qa.X = reinterpret_cast<const bf16*>(X), qa.ldx = d, qa.W = reinterpret_cast<const bf16*>(W(wqkv)), qa.ldw = d;
+      qa.d = d, qa.qkv = reinterpret_cast<bf16*>(qkv), qa.ldqkv = 3 * d, qa.o = reinterpret_cast<bf16*>(att);
+      if (qkv_attn_ok(qa)) {
+        if (stamp_on) qa.g.stamp = stamp(s, "qkv_attn " + std::to_string(g.Lq) + "x" + std::to_string(g.Lk));
+        qkv_attn_fwd(qa, s);
+        return;
+      }
+    }
+    linear(X, d, wqkv, d, qkv, 3 * d, act, M, 3 * d, d, nullptr, 0, s);
+    attf(g, att, probs, act, s);
+  }
+
   // C[M,N] = A[M,K] . W[N,K]^T  (nn.Linear)
   void linear(const void* X, int64_t ldx, int64_t woff, int64_t ldw, void* C, int64_t ldc, DType tout, int M,
               int N, int K, const float* bias, int relu, hipStream_t s) {
@@ -702,7 +728,6 @@ struct capgen_engine {
                      int layer, bool drop_on, hipStream_t s) {
     const int Me = B * N, d = L.d, He = L.He, dke = d / He;
     const float p = cfg.dropout, pa = cfg.attention_dropout;
-    linear(X, d, w.Wqkv, d, A.qkv, 3 * d, act, Me, 3 * d, d, nullptr, 0, s);
     AttnGeom g;
     g.B = B, g.H = He, g.Lq = N, g.Lk = N, g.dk = dke;
     g.q = A.qkv, g.q_ld = 3 * d, g.q_bs = (int64_t)N * 3 * d;
@@ -712,7 +737,7 @@ struct capgen_engine {
     if (valid) g.key_valid = valid, g.kv_bs = N, g.causal = 1;
     g.temperature = std::sqrt((float)dke);
     g.drop = mk_drop(pa, site(0, layer, 0), drop_on);
-    attf(g, A.att, keep_probs(g) ? A.P : nullptr, act, s);
+    self_attention(X, w.Wqkv, Me, d, g, A.qkv, A.att, keep_probs(g) ? A.P : nullptr, s);
     LnFwd l1;
     l1.M = Me, l1.d = d, l1.a = a.tmp, l1.drop = mk_drop(p, site(0, layer, 1), drop_on), l1.res = X;
     l1.gamma = P(w.ln1g), l1.beta = P(w.ln1b), l1.y = A.Y, l1.v_save = A.v1, l1.mean = A.m1, l1.rstd = A.r1;
@@ -812,7 +837,6 @@ struct capgen_engine {
     auto dec_self_half = [&](int l, void* tmp, hipStream_t fs) {
       const auto& w = L.dec[l];
       auto& A = a.dec[l];
-      linear(a.D[l], dd, w.Wqkv, dd, A.qkv, 3 * dd, act, Md, 3 * dd, dd, nullptr, 0, fs);
       AttnGeom g;
       g.B = B, g.H = Hd, g.Lq = Lq, g.Lk = Lq, g.dk = dkd;
       g.q = A.qkv, g.q_ld = 3 * dd, g.q_bs = (int64_t)Lq * 3 * dd;
@@ -822,7 +846,7 @@ struct capgen_engine {
       g.key_ids = a.ids, g.kid_bs = Lq, g.pad_idx = cfg.pad_idx, g.causal = 1;
       g.temperature = std::sqrt((float)dkd);
       g.drop = mk_drop(pa, site(1, l, 3), drop_on);
-      attf(g, A.atts, keep_probs(g) ? A.Ps : nullptr, act, fs);
+      self_attention(a.D[l], w.Wqkv, Md, dd, g, A.qkv, A.atts, keep_probs(g) ? A.Ps : nullptr, fs);
       LnFwd l1;
       l1.M = Md, l1.d = dd, l1.a = tmp, l1.drop = mk_drop(p, site(1, l, 4), drop_on), l1.res = a.D[l];
       l1.gamma = P(w.lsg), l1.beta = P(w.lsb), l1.y = A.D1, l1.v_save = A.vs, l1.mean = A.ms, l1.rstd = A.rs;
@@ -1616,7 +1640,6 @@ struct capgen_engine {
     for (int l = 0; l < L.Le; ++l) {
       const auto& w = L.enc[l];
       auto& A = a.enc[l];
-      linear(a.X[l], d, w.Wqkv, d, A.qkv, 3 * d, act, Me, 3 * d, d, nullptr, 0, s);
       AttnGeom g;
       g.B = B, g.H = He, g.Lq = N, g.Lk = N, g.dk = dke;
       g.q = A.qkv, g.q_ld = 3 * d, g.q_bs = (int64_t)N * 3 * d;
@@ -1625,7 +1648,7 @@ struct capgen_engine {
       g.o_ld = d, g.o_bs = (int64_t)N * d;
       if (cfg.encode_mask) g.key_valid = a.valid, g.kv_bs = N, g.causal = 1;
       g.temperature = std::sqrt((float)dke);
-      attf(g, A.att, nullptr, act, s);
+      self_attention(a.X[l], w.Wqkv, Me, d, g, A.qkv, A.att, nullptr, s);
       linear(A.att, d, w.Wo, d, a.tmp, d, act, Me, d, d, nullptr, 0, s);
       LnFwd l1;
       l1.M = Me, l1.d = d, l1.a = a.tmp, l1.res = a.X[l], l1.gamma = P(w.ln1g), l1.beta = P(w.ln1b), l1.y = A.Y;
@@ -2283,26 +2306,29 @@ int capgen_debug_attention(int dtype, int B, int H, int Lq, int Lk, int dk, cons
   });
 }
 
-int capgen_debug_gemm_variant(int v) {
-  return guarded([&] { gemm_set_variant(v); });
-}
-
-int capgen_debug_ffn_persist(int M, int d, int fe, const void* X, const void* W1, const float* b1, const void* W2,
-                             void* H, void* Y, int grid, int acquire, void* stream) {
+int capgen_debug_qkv_attention(int B, int L, int H, const void* X, const void* W, void* qkv, void* o,
+                               const unsigned char* key_valid, const int32_t* key_ids, int pad_idx, int causal,
+                               void* stream) {
   return guarded([&] {
-    // opt-in: an experiment kernel, not on the product path (CAPGEN_PERSIST_OK=1)
-    const char* ok = std::getenv("CAPGEN_PERSIST_OK");
-    require(ok && ok[0] == '1', "capgen_debug_ffn_persist: experiment hook, set CAPGEN_PERSIST_OK=1 to run it");
-    gemm_init();
-    GemmArgs g1, g2;
-    g1.M = M, g1.N = fe, g1.K = d, g1.A = X, g1.lda = d, g1.B = W1, g1.ldb = d, g1.C = H, g1.ldc = fe, g1.bias = b1;
-    g2.M = M, g2.N = d, g2.K = fe, g2.A = H, g2.lda = fe, g2.B = W2, g2.ldb = fe, g2.C = Y, g2.ldc = d;
-    ffn_persistent(g1, g2, grid, acquire, (hipStream_t)stream);
+    require(B >= 1 && L >= 1 && H >= 1, "debug_qkv_attention: bad shape");
+    const int d = H * 64;
+    QkvAttn qa;
+    AttnGeom& g = qa.g;
+    g.B = B, g.H = H, g.Lq = L, g.Lk = L, g.dk = 64;
+    g.q = qkv, g.q_ld = 3 * d, g.q_bs = (int64_t)L * 3 * d;
+    g.k = (const bf16*)qkv + d, g.k_ld = 3 * d, g.k_bs = (int64_t)L * 3 * d;
+    g.v = (const bf16*)qkv + 2 * d, g.v_ld = 3 * d, g.v_bs = (int64_t)L * 3 * d;
+    g.o_ld = d, g.o_bs = (int64_t)L * d;
+    g.key_valid = key_valid, g.kv_bs = L, g.key_ids = key_ids, g.kid_bs = L, g.pad_idx = pad_idx, g.causal = causal;
+    g.temperature = 8.f;  // sqrt(64)
+    qa.X = (const bf16*)X, qa.ldx = d, qa.W = (const bf16*)W, qa.ldw = d, qa.d = d;
+    qa.qkv = (bf16*)qkv, qa.ldqkv = 3 * d, qa.o = (bf16*)o;
+    qkv_attn_fwd(qa, (hipStream_t)stream);
   });
 }
 
-int capgen_debug_persist_giveups(int reset, int* out) {
-  return guarded([&] { *out = ffn_persistent_giveups(reset != 0); });
+int capgen_debug_gemm_variant(int v) {
+  return guarded([&] { gemm_set_variant(v); });
 }
 
 int capgen_debug_copy_buffer(capgen_t* h, int which, void* host_dst, int64_t bytes) {

@@ -1,6 +1,6 @@
 // capgen — the bf16 MFMA GEMM tile (LDS-DMA ring, k-loop, epilogue, in-launch split-K) as device
-// code shared by the GEMM launches (gemm_bf16.hip) and the persistent encoder-layer kernel
-// (persist.hip).  Design notes: gemm_bf16.hip header.
+// code shared by the plain and the grouped GEMM launches (gemm_bf16.hip).  Design notes:
+// gemm_bf16.hip header.
 #pragma once
 #include "gemm.h"
 

@@ -33,13 +33,6 @@ struct LnDummy {
   uint8_t valid;
 };
 __device__ LnDummy g_ln_dummy = {{}, 0, 0, 1};
-// a wave-uniform pointer the compiler must treat as an unknown SGPR value
-template <typename P>
-__device__ __forceinline__ P* opaque(P* p) {
-  uint64_t v = reinterpret_cast<uint64_t>(p);
-  asm volatile("" : "+s"(v));
-  return reinterpret_cast<P*>(v);
-}
 
 // Every global load of the row (input, residual, bias, positional row, gamma, beta, row mask,
 // dropout seed) is issued before the first store: the kernel pays ONE memory round trip (the

@@ -1,0 +1,24 @@
+// capgen — fused self-attention front: Q/K/V projection + masked attention in one launch (qkv_attn.hip).
+#pragma once
+#include "attention.h"
+
+namespace capgen {
+
+// For every (image b, head h): [q_h | k_h | v_h] = X_b . Wqkv_h^T (bf16, f32 accumulation, rounded
+// to bf16 once) into qkv, then the attention of g on them into o.  g.q/k/v must describe qkv (they
+// are what the backward reads); g.Lq == g.Lk == rows per image.
+struct QkvAttn {
+  AttnGeom g;
+  const bf16* X = nullptr;  // [B * L][ldx]
+  int64_t ldx = 0;
+  const bf16* W = nullptr;  // Wqkv [3d][ldw] (nn.Linear layout)
+  int64_t ldw = 0;
+  int d = 0;
+  bf16* qkv = nullptr;  // [B * L][ldqkv]: q | k | v
+  int64_t ldqkv = 0;
+  bf16* o = nullptr;  // attention output, g.o_ld / g.o_bs
+};
+bool qkv_attn_ok(const QkvAttn& a);
+void qkv_attn_fwd(const QkvAttn& a, hipStream_t s);
+
+}  // namespace capgen

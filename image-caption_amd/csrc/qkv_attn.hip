@@ -1,0 +1,178 @@
+// capgen — the self-attention front of a transformer block in ONE launch (bf16): the Q/K/V
+// projection of one image's rows for one head (modules.py:67-76, q_linear / k_linear / v_linear,
+// no bias) followed by that head's masked attention (modules.py:16-27, attn_mfma_dev.h).
+//
+// One workgroup of four wave64s per (image b, head h), grid B x H.  It replaces a QKV GEMM launch
+// (2304 x 1536 x 512 at C2), the dependent kernel boundary and the attention launch that re-read
+// Q / K / V from memory: the projection output goes straight into the attention's LDS images (and
+// to the qkv buffer the backward reads).
+//
+//   * the image's L <= 64 rows of X are staged in LDS once (every 16-B load issued before the first
+//     LDS write), rows padded to 16 with zeros, 16-B chunks XOR-swizzled by row (conflict-free A
+//     fragments);
+//   * wave w computes 48 of the head's 192 projection columns (q | k | v, 64 each) for all rows:
+//     its B fragments (the weight rows) are private to it, so they come straight from global
+//     memory into registers, four 32-deep k-steps per batch, double buffered (the weights are
+//     re-read by every image: L2 / Infinity-Cache hits);
+//   * v_mfma_f32_16x16x32_bf16 with swapped operands (lane = one row, 4 consecutive columns), the
+//     same k order for A and B (standard order: lane group g holds k = 8g .. 8g+7);
+//   * the f32 results are rounded to bf16 once -- exactly the values a bf16 GEMM store would leave
+//     in the qkv buffer -- and written to the buffer and to the three [64][64] LDS images;
+//   * then attn_fwd_staged (attention_mfma.hip's forward body) runs on the images.
+#include "qkv_attn.h"
+
+#include "attn_mfma_dev.h"
+#include "hazard.h"
+
+namespace capgen {
+using namespace amf;
+
+namespace {
+
+constexpr int QD = 512;       // model width handled here (K of the projection)
+constexpr int QKS = QD / 32;  // 32-deep k-steps
+constexpr int QKB = 4;        // k-steps per register batch of weight fragments
+
+__device__ __forceinline__ int xswz(int row, int chunk) { return chunk ^ (row & 15); }
+__device__ int32_t g_qa_dummy[64];  // target of the absent key-mask inputs (never used as a value)
+
+template <int LT>  // row tiles of 16 (L <= 16 LT)
+__global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
+  __shared__ __attribute__((aligned(16))) char sm[kFwdSmem];
+  __shared__ __attribute__((aligned(16))) char xs[LT * 16 * QD * 2];
+  StampScope stamp_scope(a.g.stamp);
+  if (a.g.prio) __builtin_amdgcn_s_setprio(3);
+  const AttnGeom& g = a.g;
+  const int b = blockIdx.x / g.H, h = blockIdx.x % g.H;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int L = g.Lq;  // self attention: Lq == Lk == L
+  const bf16* xb = a.X + (int64_t)b * L * a.ldx;
+
+  // ---- first weight batch, X rows (clamped row, unconditional: no load waits at a branch join),
+  // key flags; then the LDS writes: X (rows >= L zero), zeroed attention images.
+  // Projection: wave w -> columns 48w .. 48w+47 of [q_h | k_h | v_h]. ----
+  const int fr = lane & 15, fg = lane >> 4;
+  const bf16* wrow[3];
+#pragma unroll
+  for (int f = 0; f < 3; ++f) {
+    const int c = 48 * w + 16 * f + fr, which = c >> 6, within = c & 63;
+    wrow[f] = a.W + (int64_t)(which * QD + h * DK + within) * a.ldw + 8 * fg;
+  }
+  bf16x8 bq[2][QKB][3];
+#pragma unroll
+  for (int kk = 0; kk < QKB; ++kk)
+#pragma unroll
+    for (int f = 0; f < 3; ++f) bq[0][kk][f] = *reinterpret_cast<const bf16x8*>(wrow[f] + 32 * kk);
+  {
+    constexpr int CH = LT * 16 * QD / 8;  // 16-B chunks of the staged rows
+    constexpr int PER = CH / 256;
+    uint4 v[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int c = tid + 256 * u, row = c / (QD / 8), ch = c % (QD / 8);
+      v[u] = *reinterpret_cast<const uint4*>(xb + (int64_t)min(row, L - 1) * a.ldx + ch * 8);
+    }
+    // key flags (stage_key_ok's two dependent conditional loads, as one unconditional batch)
+    int kid = 0, kvl = 1;
+    if (w == 0) {
+      const int j = min(lane, L - 1);
+      kid = opaque(g.key_ids ? g.key_ids : g_qa_dummy)[g.key_ids ? (int64_t)b * g.kid_bs + j : lane];
+      kvl = opaque(g.key_valid ? g.key_valid : reinterpret_cast<const uint8_t*>(g_qa_dummy))[
+          g.key_valid ? (int64_t)b * g.kv_bs + j : lane];
+    }
+#pragma unroll
+    for (int u = 0; u < 3 * IMG / 16 / 256; ++u)
+      reinterpret_cast<uint4*>(sm)[tid + 256 * u] = uint4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int c = tid + 256 * u, row = c / (QD / 8), ch = c % (QD / 8);
+      *reinterpret_cast<uint4*>(xs + row * (QD * 2) + xswz(row, ch) * 16) = row < L ? v[u] : uint4{0u, 0u, 0u, 0u};
+    }
+    if (w == 0)
+      reinterpret_cast<unsigned char*>(sm + 3 * IMG)[lane] =
+          lane < L && (!g.key_valid || kvl != 0) && (!g.key_ids || kid != g.pad_idx);
+  }
+  f32x4 acc[LT][3];
+#pragma unroll
+  for (int i = 0; i < LT; ++i)
+#pragma unroll
+    for (int f = 0; f < 3; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();  // X staged
+#pragma unroll
+  for (int grp = 0; grp < QKS / QKB; ++grp) {
+    const int cur = grp & 1;
+    if (grp + 1 < QKS / QKB) {
+#pragma unroll
+      for (int kk = 0; kk < QKB; ++kk)
+#pragma unroll
+        for (int f = 0; f < 3; ++f)
+          bq[cur ^ 1][kk][f] = *reinterpret_cast<const bf16x8*>(wrow[f] + 32 * ((grp + 1) * QKB + kk));
+    }
+#pragma unroll
+    for (int kk = 0; kk < QKB; ++kk) {
+      const int ks = grp * QKB + kk;
+#pragma unroll
+      for (int i = 0; i < LT; ++i) {
+        const int row = 16 * i + fr;
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(xs + row * (QD * 2) + xswz(row, 4 * ks + fg) * 16);
+#pragma unroll
+        for (int f = 0; f < 3; ++f) acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[cur][kk][f], af, acc[i][f], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- bf16 results -> the qkv buffer (backward) and the LDS images (attention) ----
+  // lane holds C[row 16i + fr][col 48w + 16f + 4fg + 0..3]
+  bf16* qkvb = a.qkv + (int64_t)b * L * a.ldqkv;
+#pragma unroll
+  for (int f = 0; f < 3; ++f) {
+    const int c = 48 * w + 16 * f + 4 * fg, which = c >> 6, within = c & 63;
+    char* img = sm + which * IMG;
+#pragma unroll
+    for (int i = 0; i < LT; ++i) {
+      const int row = 16 * i + fr;
+      const f32x4 v = acc[i][f];
+      const bf16x4 r4 = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      if (row < L) {
+        *reinterpret_cast<bf16x4*>(qkvb + (int64_t)row * a.ldqkv + which * QD + h * DK + within) = r4;
+        *reinterpret_cast<bf16x4*>(img + row * 128 + swz(row, within >> 3) * 16 + (within & 7) * 2) = r4;
+      }
+    }
+  }
+  __syncthreads();
+  attn_fwd_staged(g, a.o, nullptr, b, h, sm);
+}
+
+}  // namespace
+
+bool qkv_attn_ok(const QkvAttn& a) {
+  const AttnGeom& g = a.g;
+  return g.dk == DK && g.H * DK == QD && a.d == QD && g.Lq == g.Lk && g.Lq >= 1 && g.Lq <= 64 && g.kv_bmod == 0 &&
+         !g.kv_row && a.ldx % 8 == 0 && a.ldw % 8 == 0 && a.ldqkv % 8 == 0 && g.o_ld % 8 == 0 && g.o_bs % 8 == 0;
+}
+
+void qkv_attn_fwd(const QkvAttn& a, hipStream_t s) {
+  require(qkv_attn_ok(a), "qkv_attn_fwd: unsupported geometry (head size 64, d = 512, self attention, L <= 64)");
+  const AttnGeom& g = a.g;
+  if (hz::active()) {
+    using namespace hz;
+    const int L = g.Lq;
+    const Rgn r[] = {rows_blk(a.X, g.B, L, (int64_t)L * a.ldx, a.ldx, a.d, 2, RD), rd(a.W, (int64_t)3 * a.d * a.ldw * 2),
+                     blk(g.key_valid, g.B, L, g.kv_bs, RD), blk(g.key_ids, g.B, (int64_t)L * 4, g.kid_bs * 4, RD),
+                     rd(g.drop.seed_ptr, 8), rows_blk(a.qkv, g.B, L, (int64_t)L * a.ldqkv, a.ldqkv, 3 * a.d, 2, WR),
+                     rows_blk(a.o, g.B, L, g.o_bs, g.o_ld, a.d, 2, WR)};
+    op(s, "qkv_attn", r, sizeof r / sizeof r[0]);
+  }
+  const int lt = (a.g.Lq + 15) / 16;
+  const dim3 grid(a.g.B * a.g.H);
+  switch (lt) {
+    case 1: qkv_attn_kernel<1><<<grid, 256, 0, s>>>(a); break;
+    case 2: qkv_attn_kernel<2><<<grid, 256, 0, s>>>(a); break;
+    case 3: qkv_attn_kernel<3><<<grid, 256, 0, s>>>(a); break;
+    default: qkv_attn_kernel<4><<<grid, 256, 0, s>>>(a); break;
+  }
+  CAPGEN_HIP(hipGetLastError());
+}
+
+}  // namespace capgen

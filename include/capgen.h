@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define CAPGEN_ABI_VERSION 6
+#define CAPGEN_ABI_VERSION 7
 
 typedef struct capgen_engine capgen_t;
 
@@ -145,13 +145,6 @@ int capgen_debug_gemm(int M, int N, int K, const void* A, int64_t lda, int ta, c
 
 /* Experiment hook: force a GEMM tile/wave/pipeline variant (0 = production heuristic). */
 int capgen_debug_gemm_variant(int variant);
-/* Experiment (persist.hip): the FFN pair H = relu(X.W1^T + b1) [M, fe], Y = H.W2^T [M, d] (bf16,
- * weights [out][in]) as ONE persistent launch of `grid` workgroups with row-block dependency
- * counters; acquire = 0 drops the consumer's agent acquire (diagnostic). */
-int capgen_debug_ffn_persist(int M, int d, int fe, const void* X, const void* W1, const float* b1, const void* W2,
-                             void* H, void* Y, int grid, int acquire, void* stream);
-/* Persistent-launch spins that gave up (0 in a correct run); synchronises; reset != 0 zeroes. */
-int capgen_debug_persist_giveups(int reset, int* out);
 /* Diagnostic hook: the in-launch split-K combine's hand-off protocol (0 = the production form:
  * sc1 slab stores, agent acquire + plain slab loads in the combining workgroup, tickets re-armed
  * by the last arriver's atomic exchange).  Bits: 1 adds a writer release fence, 2 drops the
@@ -216,6 +209,14 @@ int capgen_scst_rewards(const int64_t* target, int64_t target_ld, const int64_t*
 int capgen_debug_attention(int dtype, int B, int H, int Lq, int Lk, int dk, const void* q, const void* k,
                            const void* v, const unsigned char* key_valid, int causal, float temperature, void* o,
                            float* probs, const void* dout, void* dq, void* dk_, void* dv, void* stream);
+
+/* Test hook: the fused self-attention front (qkv_attn.hip; modules.py:67-76 then 16-27), bf16:
+ * qkv [B*L, 3*H*64] = X [B*L, H*64] . W^T (W = [q; k; v] weights [3*H*64, H*64]), then the masked
+ * attention of every (image, head) into o [B*L, H*64].  key_valid [B][L] bytes / key_ids [B][L]
+ * int32 (== pad_idx: masked) optional; causal masks keys j > i.  Head size 64, H*64 = 512 only. */
+int capgen_debug_qkv_attention(int B, int L, int H, const void* X, const void* W, void* qkv, void* o,
+                               const unsigned char* key_valid, const int32_t* key_ids, int pad_idx, int causal,
+                               void* stream);
 
 /* Persisted GEMM autotune table (no reference counterpart: the reference's GEMMs are cuBLAS calls
  * of torch eager, models.py:120-126).  The bf16 GEMM picks a tile / wave / pipeline / split-K

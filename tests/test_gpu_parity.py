@@ -933,6 +933,57 @@ def test_attention_kernels_vs_torch(dtype, B, H, Lq, Lk, dk, causal, mask):
         assert err < tol, (name, err)
 
 
+@pytest.mark.parametrize("B,L,mask", [(4, 36, "none"), (3, 36, "valid_causal"), (5, 19, "ids_causal"), (2, 1, "none"),
+                                       (2, 64, "valid_causal"), (3, 48, "ids_causal"), (64, 36, "none")])
+def test_fused_qkv_attention_vs_torch(B, L, mask):
+    """The fused self-attention front (qkv_attn.hip: Q/K/V projection straight into the attention's LDS
+    images) vs torch on the same bf16 inputs: qkv within bf16 rounding of the f32 product (a different
+    summation order can flip the last bit of a rounded element), attention output within the bf16 MFMA
+    attention tolerance (test_attention_kernels_vs_torch), at the encoder (36 rows, key-valid + causal
+    with encode_mask), decoder self-attention (19 rows, key ids + causal) and edge row counts."""
+    import ctypes as C
+    from capgen import _lib
+    lib = _lib.load()
+    H, d = 8, 512
+    g = torch.Generator(device="cpu").manual_seed(B * 131 + L)
+    X = (torch.randn(B * L, d, generator=g) * 0.5).to(torch.bfloat16)
+    W = (torch.randn(3 * d, d, generator=g) / d ** 0.5).to(torch.bfloat16)
+    valid = torch.ones(B, L, dtype=torch.uint8)
+    ids = torch.randint(3, 100, (B, L), generator=g, dtype=torch.int32)
+    for b in range(B):
+        if mask == "valid_causal":
+            valid[b, max(1, L - 3 * b - 2):] = 0
+        if mask == "ids_causal":
+            ids[b, max(1, L - 2 * b - 1):] = 0
+    qkv_ref = (X.float() @ W.float().t())
+    q, k, v = (qkv_ref.bfloat16().float().view(B, L, 3, H, 64)[:, :, i].transpose(1, 2) for i in range(3))
+    s = (q / 8.0) @ k.transpose(-1, -2)
+    m = torch.zeros(B, 1, L, L, dtype=torch.bool)
+    if mask == "valid_causal":
+        m = m | (valid[:, None, None, :] == 0)
+    if mask == "ids_causal":
+        m = m | (ids[:, None, None, :] == 0)
+    if mask != "none":
+        m = m | torch.triu(torch.ones(L, L, dtype=torch.bool), 1)[None, None]
+    o_ref = (torch.softmax(s.masked_fill(m, float("-inf")), -1) @ v).transpose(1, 2).reshape(B * L, d)
+    Xd, Wd = X.to(DEV), W.to(DEV)
+    qkv = torch.empty(B * L, 3 * d, device=DEV, dtype=torch.bfloat16)
+    o = torch.empty(B * L, d, device=DEV, dtype=torch.bfloat16)
+    vd, idd = valid.to(DEV), ids.to(DEV)
+    ptr = lambda t: C.c_void_p(t.data_ptr())
+    _lib.check(lib.capgen_debug_qkv_attention(B, L, H, ptr(Xd), ptr(Wd), ptr(qkv), ptr(o),
+                                              ptr(vd) if mask == "valid_causal" else None,
+                                              ptr(idd) if mask == "ids_causal" else None, 0,
+                                              int(mask != "none"), None))
+    torch.cuda.synchronize()
+    got = qkv.float().cpu()
+    # each element: the bf16 rounding of the f32 product, or its neighbour (summation-order tie)
+    ulp = (qkv_ref.abs() * 2.0 ** -7).clamp_min(1e-5)  # (+ the f32 sums' own order noise near 0)
+    assert ((got - qkv_ref).abs() <= ulp).all(), float(((got - qkv_ref).abs() / ulp).max())
+    err = (o.float().cpu() - o_ref).abs().max().item() / o_ref.abs().max().item()
+    assert err < 3e-2, err
+
+
 def _rl_engine(tag, dtype="fp32"):
     from capgen.engine import Engine
     cfg, seed, z = load_fixture(tag)
