@@ -82,6 +82,7 @@ _SIGS = {
     "capgen_debug_attention": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P,
                                          C.c_int, C.c_float, _P, _P, _P, _P, _P, _P, _P]),
     "capgen_debug_qkv_attention": (C.c_int, [C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, C.c_int, C.c_int, _P]),
+    "capgen_debug_cross_attention": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P]),
     "capgen_dp_unique_id": (C.c_int, [C.c_char_p]),
     "capgen_dp_init": (C.c_int, [_P, C.c_char_p, C.c_int, C.c_int]),
     "capgen_dp_set_global_count": (C.c_int, [_P, C.c_float]),

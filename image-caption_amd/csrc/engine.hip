@@ -414,6 +414,27 @@ struct capgen_engine {
     attf(g, att, probs, act, s);
   }
 
+  // The cross-attention of a decoder block (modules.py:195-197): q = D1 . Wq^T then attention over
+  // the precomputed cross K/V.  q_done: q already projected (else bf16: the fused launch projects it
+  // straight into the attention's LDS image, qkv_attn.hip cross mode).
+  bool cross_fusable(int Lq) const {
+    return fused_qkv_on && act == DType::BF16 && L.dd == 512 && L.Hd * 64 == L.dd && Lq >= 1 && Lq <= 64;
+  }
+  void cross_attention(const AttnGeom& c, const void* D1, int64_t wq, int d, void* qc, void* attc, float* probs,
+                       bool q_done, hipStream_t s) {
+    if (!q_done) {
+      QkvAttn qa;
+      qa.g = c, qa.g.prio = prio(s), qa.cross = 1;
+      qa.X = reinterpret_cast<const bf16*>(D1), qa.ldx = d, qa.W = reinterpret_cast<const bf16*>(W(wq)), qa.ldw = d;
+      qa.d = d, qa.qkv = reinterpret_cast<bf16*>(qc), qa.ldqkv = d, qa.o = reinterpret_cast<bf16*>(attc);
+      require(!probs && qkv_attn_ok(qa), "internal: cross-attention geometry the fused launch does not take");
+      if (stamp_on) qa.g.stamp = stamp(s, "qkv_attn cross " + std::to_string(c.Lq) + "x" + std::to_string(c.Lk));
+      qkv_attn_fwd(qa, s);
+      return;
+    }
+    attf(c, attc, probs, act, s);
+  }
+
   // C[M,N] = A[M,K] . W[N,K]^T  (nn.Linear)
   void linear(const void* X, int64_t ldx, int64_t woff, int64_t ldw, void* C, int64_t ldc, DType tout, int M,
               int N, int K, const float* bias, int relu, hipStream_t s) {
@@ -834,7 +855,8 @@ struct capgen_engine {
       linear_ln(a.E, L.dwe, L.Wel, L.dwe, Md, dd, L.dwe, ln, fs);
     };
     // self attention: key-pad(ids) OR causal (model.py:421-430), then the cross-attention query
-    auto dec_self_half = [&](int l, void* tmp, hipStream_t fs) {
+    // q_proj: also the cross-attention query projection (else the fused cross-attention launch does it)
+    auto dec_self_half = [&](int l, void* tmp, hipStream_t fs, bool q_proj) {
       const auto& w = L.dec[l];
       auto& A = a.dec[l];
       AttnGeom g;
@@ -851,14 +873,14 @@ struct capgen_engine {
       l1.M = Md, l1.d = dd, l1.a = tmp, l1.drop = mk_drop(p, site(1, l, 4), drop_on), l1.res = a.D[l];
       l1.gamma = P(w.lsg), l1.beta = P(w.lsb), l1.y = A.D1, l1.v_save = A.vs, l1.mean = A.ms, l1.rstd = A.rs;
       linear_ln(A.atts, dd, w.Wo_s, dd, Md, dd, dd, l1, fs);
-      linear(A.D1, dd, w.Wq_c, dd, A.qc, dd, act, Md, dd, dd, nullptr, 0, fs);
+      if (q_proj) linear(A.D1, dd, w.Wq_c, dd, A.qc, dd, act, Md, dd, dd, nullptr, 0, fs);
     };
     if (front) {
       if (cap_split) cap_cut(s, 0, es2);
       else dep(s, es2, ev_ff);
       if (caps_front) prepare_captions(caps, B, T, cfg.pad_idx, a.ids, a.tgt, a.count, es2);
       dec_embed(a.tmpf, es2);
-      dec_self_half(0, a.tmpf, es2);
+      dec_self_half(0, a.tmpf, es2, true);
       if (cap_split) cap_cut(es2, 1, s);
       else hz::record(ev_fj, es2);
     }
@@ -885,7 +907,8 @@ struct capgen_engine {
     for (int l = 0; l < L.Ld; ++l) {
       const auto& w = L.dec[l];
       auto& A = a.dec[l];
-      if (!(front && l == 0)) dec_self_half(l, a.tmp, s);
+      const bool q_done = front && l == 0;  // block 0's query was projected on es2 with the front
+      if (!q_done) dec_self_half(l, a.tmp, s, !cross_fusable(Lq));
       // cross attention over the encoder output, context mask = region key-pad (model.py:82)
       AttnGeom c;
       c.B = B, c.H = Hd, c.Lq = Lq, c.Lk = N, c.dk = dkd;
@@ -896,7 +919,7 @@ struct capgen_engine {
       c.key_valid = a.valid, c.kv_bs = N;
       c.temperature = std::sqrt((float)dkd);
       c.drop = mk_drop(pa, site(1, l, 5), drop_on);
-      attf(c, A.attc, keep_probs(c) ? A.Pc : nullptr, act, s);
+      cross_attention(c, A.D1, w.Wq_c, dd, A.qc, A.attc, keep_probs(c) ? A.Pc : nullptr, q_done || !cross_fusable(Lq), s);
       LnFwd l2;
       l2.M = Md, l2.d = dd, l2.a = a.tmp, l2.drop = mk_drop(p, site(1, l, 6), drop_on), l2.res = A.D1;
       l2.gamma = P(w.lcg), l2.beta = P(w.lcb), l2.y = A.D2, l2.v_save = A.vc, l2.mean = A.mc, l2.rstd = A.rc;
@@ -2323,6 +2346,27 @@ int capgen_debug_qkv_attention(int B, int L, int H, const void* X, const void* W
     g.temperature = 8.f;  // sqrt(64)
     qa.X = (const bf16*)X, qa.ldx = d, qa.W = (const bf16*)W, qa.ldw = d, qa.d = d;
     qa.qkv = (bf16*)qkv, qa.ldqkv = 3 * d, qa.o = (bf16*)o;
+    qkv_attn_fwd(qa, (hipStream_t)stream);
+  });
+}
+
+int capgen_debug_cross_attention(int B, int Lq, int Lk, int H, const void* X, const void* Wq, const void* KV, void* q,
+                                 void* o, const unsigned char* key_valid, void* stream) {
+  return guarded([&] {
+    require(B >= 1 && Lq >= 1 && Lk >= 1 && H >= 1, "debug_cross_attention: bad shape");
+    const int d = H * 64;
+    QkvAttn qa;
+    AttnGeom& g = qa.g;
+    g.B = B, g.H = H, g.Lq = Lq, g.Lk = Lk, g.dk = 64;
+    g.q = q, g.q_ld = d, g.q_bs = (int64_t)Lq * d;
+    g.k = KV, g.k_ld = 2 * d, g.k_bs = (int64_t)Lk * 2 * d;
+    g.v = (const bf16*)KV + d, g.v_ld = 2 * d, g.v_bs = (int64_t)Lk * 2 * d;
+    g.o_ld = d, g.o_bs = (int64_t)Lq * d;
+    g.key_valid = key_valid, g.kv_bs = Lk;
+    g.temperature = 8.f;
+    qa.cross = 1;
+    qa.X = (const bf16*)X, qa.ldx = d, qa.W = (const bf16*)Wq, qa.ldw = d, qa.d = d;
+    qa.qkv = (bf16*)q, qa.ldqkv = d, qa.o = (bf16*)o;
     qkv_attn_fwd(qa, (hipStream_t)stream);
   });
 }

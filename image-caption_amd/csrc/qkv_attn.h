@@ -4,7 +4,7 @@
 
 namespace capgen {
 
-// For every (image b, head h): [q_h | k_h | v_h] = X_b . Wqkv_h^T (bf16, f32 accumulation, rounded
+// For every (image b, head h): [q_h | k_h | v_h] = X_b . Wqkv_h^T (cross: q_h only) (bf16, f32 accumulation, rounded
 // to bf16 once) into qkv, then the attention of g on them into o.  g.q/k/v must describe qkv (they
 // are what the backward reads); g.Lq == g.Lk == rows per image.
 struct QkvAttn {
@@ -17,6 +17,9 @@ struct QkvAttn {
   bf16* qkv = nullptr;  // [B * L][ldqkv]: q | k | v
   int64_t ldqkv = 0;
   bf16* o = nullptr;  // attention output, g.o_ld / g.o_bs
+  // cross attention (DecoderBlock's second MHA, modules.py:195-197): only q = X . Wq^T is projected
+  // (W = Wq [d][d], qkv = the q buffer); K / V come from g.k / g.v (the precomputed cross K/V)
+  int cross = 0;
 };
 bool qkv_attn_ok(const QkvAttn& a);
 void qkv_attn_fwd(const QkvAttn& a, hipStream_t s);

@@ -36,7 +36,9 @@ constexpr int QKB = 4;        // k-steps per register batch of weight fragments
 __device__ __forceinline__ int xswz(int row, int chunk) { return chunk ^ (row & 15); }
 __device__ int32_t g_qa_dummy[64];  // target of the absent key-mask inputs (never used as a value)
 
-template <int LT>  // row tiles of 16 (L <= 16 LT)
+// NP = 3: self attention, q | k | v all projected from X (L = Lq = Lk rows);
+// NP = 1: cross attention, only q projected (Lq rows of X), K / V staged from g.k / g.v (Lk rows)
+template <int LT, int NP>  // LT: query-row tiles of 16 (Lq <= 16 LT)
 __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
   __shared__ __attribute__((aligned(16))) char sm[kFwdSmem];
   __shared__ __attribute__((aligned(16))) char xs[LT * 16 * QD * 2];
@@ -46,24 +48,25 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
   const int b = blockIdx.x / g.H, h = blockIdx.x % g.H;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int L = g.Lq;  // self attention: Lq == Lk == L
+  constexpr int NF = NP;  // 16-column fragments per wave (48 or 16 of the 64 NP columns)
+  const int L = g.Lq;     // rows of X (query rows)
   const bf16* xb = a.X + (int64_t)b * L * a.ldx;
 
   // ---- first weight batch, X rows (clamped row, unconditional: no load waits at a branch join),
   // key flags; then the LDS writes: X (rows >= L zero), zeroed attention images.
   // Projection: wave w -> columns 48w .. 48w+47 of [q_h | k_h | v_h]. ----
   const int fr = lane & 15, fg = lane >> 4;
-  const bf16* wrow[3];
+  const bf16* wrow[NF];
 #pragma unroll
-  for (int f = 0; f < 3; ++f) {
-    const int c = 48 * w + 16 * f + fr, which = c >> 6, within = c & 63;
+  for (int f = 0; f < NF; ++f) {
+    const int c = 16 * NF * w + 16 * f + fr, which = c >> 6, within = c & 63;
     wrow[f] = a.W + (int64_t)(which * QD + h * DK + within) * a.ldw + 8 * fg;
   }
-  bf16x8 bq[2][QKB][3];
+  bf16x8 bq[2][QKB][NF];
 #pragma unroll
   for (int kk = 0; kk < QKB; ++kk)
 #pragma unroll
-    for (int f = 0; f < 3; ++f) bq[0][kk][f] = *reinterpret_cast<const bf16x8*>(wrow[f] + 32 * kk);
+    for (int f = 0; f < NF; ++f) bq[0][kk][f] = *reinterpret_cast<const bf16x8*>(wrow[f] + 32 * kk);
   {
     constexpr int CH = LT * 16 * QD / 8;  // 16-B chunks of the staged rows
     constexpr int PER = CH / 256;
@@ -73,31 +76,57 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
       const int c = tid + 256 * u, row = c / (QD / 8), ch = c % (QD / 8);
       v[u] = *reinterpret_cast<const uint4*>(xb + (int64_t)min(row, L - 1) * a.ldx + ch * 8);
     }
+    // cross attention: K / V head slices from memory (rows < Lk, clamped, unconditional)
+    uint4 kv[2][2];
+    if constexpr (NP == 1) {
+      const int bk = g.kv_bmod ? b % g.kv_bmod : b;
+      const bf16* src[2] = {reinterpret_cast<const bf16*>(g.k) + (int64_t)bk * g.k_bs + h * DK,
+                            reinterpret_cast<const bf16*>(g.v) + (int64_t)bk * g.v_bs + h * DK};
+      const int64_t ld[2] = {g.k_ld, g.v_ld};
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int c = tid + 256 * u, row = c >> 3, ch = c & 7;
+          kv[i][u] = *reinterpret_cast<const uint4*>(src[i] + (int64_t)min(row, g.Lk - 1) * ld[i] + ch * 8);
+        }
+    }
     // key flags (stage_key_ok's two dependent conditional loads, as one unconditional batch)
     int kid = 0, kvl = 1;
     if (w == 0) {
-      const int j = min(lane, L - 1);
+      const int j = min(lane, g.Lk - 1);
+      const int bk = g.kv_bmod ? b % g.kv_bmod : b;
       kid = opaque(g.key_ids ? g.key_ids : g_qa_dummy)[g.key_ids ? (int64_t)b * g.kid_bs + j : lane];
       kvl = opaque(g.key_valid ? g.key_valid : reinterpret_cast<const uint8_t*>(g_qa_dummy))[
-          g.key_valid ? (int64_t)b * g.kv_bs + j : lane];
+          g.key_valid ? (int64_t)bk * g.kv_bs + j : lane];
     }
 #pragma unroll
-    for (int u = 0; u < 3 * IMG / 16 / 256; ++u)
+    for (int u = 0; u < NP * IMG / 16 / 256; ++u)
       reinterpret_cast<uint4*>(sm)[tid + 256 * u] = uint4{0u, 0u, 0u, 0u};
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int c = tid + 256 * u, row = c / (QD / 8), ch = c % (QD / 8);
       *reinterpret_cast<uint4*>(xs + row * (QD * 2) + xswz(row, ch) * 16) = row < L ? v[u] : uint4{0u, 0u, 0u, 0u};
     }
+    if constexpr (NP == 1) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int c = tid + 256 * u, row = c >> 3, ch = c & 7;
+          *reinterpret_cast<uint4*>(sm + (1 + i) * IMG + row * 128 + swz(row, ch) * 16) =
+              row < g.Lk ? kv[i][u] : uint4{0u, 0u, 0u, 0u};
+        }
+    }
     if (w == 0)
       reinterpret_cast<unsigned char*>(sm + 3 * IMG)[lane] =
-          lane < L && (!g.key_valid || kvl != 0) && (!g.key_ids || kid != g.pad_idx);
+          lane < g.Lk && (!g.key_valid || kvl != 0) && (!g.key_ids || kid != g.pad_idx);
   }
-  f32x4 acc[LT][3];
+  f32x4 acc[LT][NF];
 #pragma unroll
   for (int i = 0; i < LT; ++i)
 #pragma unroll
-    for (int f = 0; f < 3; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int f = 0; f < NF; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();  // X staged
 #pragma unroll
   for (int grp = 0; grp < QKS / QKB; ++grp) {
@@ -106,7 +135,7 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
 #pragma unroll
       for (int kk = 0; kk < QKB; ++kk)
 #pragma unroll
-        for (int f = 0; f < 3; ++f)
+        for (int f = 0; f < NF; ++f)
           bq[cur ^ 1][kk][f] = *reinterpret_cast<const bf16x8*>(wrow[f] + 32 * ((grp + 1) * QKB + kk));
     }
 #pragma unroll
@@ -117,17 +146,17 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
         const int row = 16 * i + fr;
         const bf16x8 af = *reinterpret_cast<const bf16x8*>(xs + row * (QD * 2) + xswz(row, 4 * ks + fg) * 16);
 #pragma unroll
-        for (int f = 0; f < 3; ++f) acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[cur][kk][f], af, acc[i][f], 0, 0, 0);
+        for (int f = 0; f < NF; ++f) acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[cur][kk][f], af, acc[i][f], 0, 0, 0);
       }
     }
   }
 
   // ---- bf16 results -> the qkv buffer (backward) and the LDS images (attention) ----
-  // lane holds C[row 16i + fr][col 48w + 16f + 4fg + 0..3]
+  // lane holds C[row 16i + fr][col 16 NF w + 16f + 4fg + 0..3]
   bf16* qkvb = a.qkv + (int64_t)b * L * a.ldqkv;
 #pragma unroll
-  for (int f = 0; f < 3; ++f) {
-    const int c = 48 * w + 16 * f + 4 * fg, which = c >> 6, within = c & 63;
+  for (int f = 0; f < NF; ++f) {
+    const int c = 16 * NF * w + 16 * f + 4 * fg, which = c >> 6, within = c & 63;
     char* img = sm + which * IMG;
 #pragma unroll
     for (int i = 0; i < LT; ++i) {
@@ -148,8 +177,11 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
 
 bool qkv_attn_ok(const QkvAttn& a) {
   const AttnGeom& g = a.g;
-  return g.dk == DK && g.H * DK == QD && a.d == QD && g.Lq == g.Lk && g.Lq >= 1 && g.Lq <= 64 && g.kv_bmod == 0 &&
-         !g.kv_row && a.ldx % 8 == 0 && a.ldw % 8 == 0 && a.ldqkv % 8 == 0 && g.o_ld % 8 == 0 && g.o_bs % 8 == 0;
+  const bool shape = a.cross ? (g.Lk >= 1 && g.Lk <= 64 && g.k_ld % 8 == 0 && g.v_ld % 8 == 0 && g.k_bs % 8 == 0 &&
+                                g.v_bs % 8 == 0)
+                             : (g.Lq == g.Lk && g.kv_bmod == 0);
+  return shape && g.dk == DK && g.H * DK == QD && a.d == QD && g.Lq >= 1 && g.Lq <= 64 && !g.kv_row &&
+         a.ldx % 8 == 0 && a.ldw % 8 == 0 && a.ldqkv % 8 == 0 && g.o_ld % 8 == 0 && g.o_bs % 8 == 0;
 }
 
 void qkv_attn_fwd(const QkvAttn& a, hipStream_t s) {
@@ -158,19 +190,31 @@ void qkv_attn_fwd(const QkvAttn& a, hipStream_t s) {
   if (hz::active()) {
     using namespace hz;
     const int L = g.Lq;
-    const Rgn r[] = {rows_blk(a.X, g.B, L, (int64_t)L * a.ldx, a.ldx, a.d, 2, RD), rd(a.W, (int64_t)3 * a.d * a.ldw * 2),
-                     blk(g.key_valid, g.B, L, g.kv_bs, RD), blk(g.key_ids, g.B, (int64_t)L * 4, g.kid_bs * 4, RD),
-                     rd(g.drop.seed_ptr, 8), rows_blk(a.qkv, g.B, L, (int64_t)L * a.ldqkv, a.ldqkv, 3 * a.d, 2, WR),
+    const int np = a.cross ? 1 : 3, Bk = g.kv_bmod > 0 ? std::min(g.B, g.kv_bmod) : g.B;
+    const Rgn r[] = {rows_blk(a.X, g.B, L, (int64_t)L * a.ldx, a.ldx, a.d, 2, RD), rd(a.W, (int64_t)np * a.d * a.ldw * 2),
+                     blk(g.key_valid, Bk, g.Lk, g.kv_bs, RD), blk(g.key_ids, g.B, (int64_t)g.Lk * 4, g.kid_bs * 4, RD),
+                     rows_blk(a.cross ? g.k : nullptr, Bk, g.Lk, g.k_bs, g.k_ld, a.d, 2, RD),
+                     rows_blk(a.cross ? g.v : nullptr, Bk, g.Lk, g.v_bs, g.v_ld, a.d, 2, RD),
+                     rd(g.drop.seed_ptr, 8), rows_blk(a.qkv, g.B, L, (int64_t)L * a.ldqkv, a.ldqkv, np * a.d, 2, WR),
                      rows_blk(a.o, g.B, L, g.o_bs, g.o_ld, a.d, 2, WR)};
     op(s, "qkv_attn", r, sizeof r / sizeof r[0]);
   }
   const int lt = (a.g.Lq + 15) / 16;
   const dim3 grid(a.g.B * a.g.H);
-  switch (lt) {
-    case 1: qkv_attn_kernel<1><<<grid, 256, 0, s>>>(a); break;
-    case 2: qkv_attn_kernel<2><<<grid, 256, 0, s>>>(a); break;
-    case 3: qkv_attn_kernel<3><<<grid, 256, 0, s>>>(a); break;
-    default: qkv_attn_kernel<4><<<grid, 256, 0, s>>>(a); break;
+  if (a.cross) {
+    switch (lt) {
+      case 1: qkv_attn_kernel<1, 1><<<grid, 256, 0, s>>>(a); break;
+      case 2: qkv_attn_kernel<2, 1><<<grid, 256, 0, s>>>(a); break;
+      case 3: qkv_attn_kernel<3, 1><<<grid, 256, 0, s>>>(a); break;
+      default: qkv_attn_kernel<4, 1><<<grid, 256, 0, s>>>(a); break;
+    }
+  } else {
+    switch (lt) {
+      case 1: qkv_attn_kernel<1, 3><<<grid, 256, 0, s>>>(a); break;
+      case 2: qkv_attn_kernel<2, 3><<<grid, 256, 0, s>>>(a); break;
+      case 3: qkv_attn_kernel<3, 3><<<grid, 256, 0, s>>>(a); break;
+      default: qkv_attn_kernel<4, 3><<<grid, 256, 0, s>>>(a); break;
+    }
   }
   CAPGEN_HIP(hipGetLastError());
 }

@@ -218,6 +218,12 @@ int capgen_debug_qkv_attention(int B, int L, int H, const void* X, const void* W
                                const unsigned char* key_valid, const int32_t* key_ids, int pad_idx, int causal,
                                void* stream);
 
+/* Test hook: the fused cross-attention front (qkv_attn.hip cross mode; modules.py:195-197), bf16:
+ * q [B*Lq, H*64] = X . Wq^T, then attention over K / V = KV [B*Lk, 2*H*64] (k | v per row) with the
+ * key mask key_valid [B][Lk] (optional) into o [B*Lq, H*64].  Head size 64, H*64 = 512 only. */
+int capgen_debug_cross_attention(int B, int Lq, int Lk, int H, const void* X, const void* Wq, const void* KV, void* q,
+                                 void* o, const unsigned char* key_valid, void* stream);
+
 /* Persisted GEMM autotune table (no reference counterpart: the reference's GEMMs are cuBLAS calls
  * of torch eager, models.py:120-126).  The bf16 GEMM picks a tile / wave / pipeline / split-K
  * variant per shape by timing; a table file fixes those choices so that every process (bench,

@@ -934,7 +934,8 @@ def test_attention_kernels_vs_torch(dtype, B, H, Lq, Lk, dk, causal, mask):
 
 
 @pytest.mark.parametrize("B,L,mask", [(4, 36, "none"), (3, 36, "valid_causal"), (5, 19, "ids_causal"), (2, 1, "none"),
-                                       (2, 64, "valid_causal"), (3, 48, "ids_causal"), (64, 36, "none")])
+                                       (2, 64, "valid_causal"), (3, 48, "ids_causal"), (64, 36, "none"),
+                                       (4, 19, "cross36"), (3, 1, "cross36"), (64, 19, "cross36"), (2, 64, "cross64")])
 def test_fused_qkv_attention_vs_torch(B, L, mask):
     """The fused self-attention front (qkv_attn.hip: Q/K/V projection straight into the attention's LDS
     images) vs torch on the same bf16 inputs: qkv within bf16 rounding of the f32 product (a different
@@ -948,6 +949,31 @@ def test_fused_qkv_attention_vs_torch(B, L, mask):
     g = torch.Generator(device="cpu").manual_seed(B * 131 + L)
     X = (torch.randn(B * L, d, generator=g) * 0.5).to(torch.bfloat16)
     W = (torch.randn(3 * d, d, generator=g) / d ** 0.5).to(torch.bfloat16)
+    if mask.startswith("cross"):  # decoder cross attention: q projected, K / V given (key-valid mask)
+        Lk = int(mask[5:])
+        Wq = W[:d].contiguous()
+        KV = (torch.randn(B * Lk, 2 * d, generator=g)).to(torch.bfloat16)
+        kvalid = torch.ones(B, Lk, dtype=torch.uint8)
+        for b in range(B):
+            kvalid[b, max(1, Lk - 5 * b - 3):] = 0
+        q_ref = X.float() @ Wq.float().t()
+        q = q_ref.bfloat16().float().view(B, L, H, 64).transpose(1, 2)
+        k, v = (KV.float().view(B, Lk, 2, H, 64)[:, :, i].transpose(1, 2) for i in range(2))
+        s = (q / 8.0) @ k.transpose(-1, -2)
+        s = s.masked_fill((kvalid[:, None, None, :] == 0), float("-inf"))
+        o_ref = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B * L, d)
+        qd = torch.empty(B * L, d, device=DEV, dtype=torch.bfloat16)
+        o = torch.empty(B * L, d, device=DEV, dtype=torch.bfloat16)
+        Xd, Wd, KVd, vd = X.to(DEV), Wq.to(DEV), KV.to(DEV), kvalid.to(DEV)
+        ptr = lambda t: C.c_void_p(t.data_ptr())
+        _lib.check(lib.capgen_debug_cross_attention(B, L, Lk, H, ptr(Xd), ptr(Wd), ptr(KVd), ptr(qd), ptr(o), ptr(vd),
+                                                    None))
+        torch.cuda.synchronize()
+        ulp = (q_ref.abs() * 2.0 ** -7).clamp_min(1e-5)
+        assert ((qd.float().cpu() - q_ref).abs() <= ulp).all()
+        err = (o.float().cpu() - o_ref).abs().max().item() / o_ref.abs().max().item()
+        assert err < 3e-2, err
+        return
     valid = torch.ones(B, L, dtype=torch.uint8)
     ids = torch.randint(3, 100, (B, L), generator=g, dtype=torch.int32)
     for b in range(B):
