@@ -1777,17 +1777,41 @@ struct capgen_engine {
       LnFwd l1;
       l1.M = R, l1.d = dd, l1.a = g.tmp, l1.res = g.x, l1.gamma = P(w.lsg), l1.beta = P(w.lsb), l1.y = g.x1;
       lnf(l1, s);
-      linear(g.x1, dd, w.Wq_c, dd, g.q, dd, act, R, dd, dd, nullptr, 0, s);
-      AttnGeom c;
-      c.B = R, c.H = Hd, c.Lq = 1, c.Lk = N, c.dk = dkd;
-      c.q = g.q, c.q_ld = dd, c.q_bs = dd;
-      c.k = at(a.KV, (int64_t)l * 2 * dd), c.k_ld = kvld, c.k_bs = (int64_t)N * kvld;
-      c.v = at(a.KV, (int64_t)l * 2 * dd + dd), c.v_ld = kvld, c.v_bs = (int64_t)N * kvld;
-      c.kv_bmod = Bimg;
-      c.o_ld = dd, c.o_bs = dd;
-      c.key_valid = a.valid, c.kv_bs = N;
-      c.temperature = std::sqrt((float)dkd);
-      attf(c, g.att, (want_attn && l == L.Ld - 1) ? g.Pc : nullptr, act, s);
+      const bool want_p = want_attn && l == L.Ld - 1;
+      const int kb = R / Bimg;  // rows per image (beams): row r = j * Bimg + image
+      if (!want_p && R % Bimg == 0 && cross_fusable(kb)) {
+        // the query projection and the cross attention of every image's kb rows in one launch
+        // (qkv_attn.hip cross mode, one workgroup per (image, head); the query is not stored)
+        QkvAttn qa;
+        AttnGeom& c = qa.g;
+        c.B = Bimg, c.H = Hd, c.Lq = kb, c.Lk = N, c.dk = dkd;
+        c.q = g.q, c.q_ld = (int64_t)Bimg * dd, c.q_bs = dd;
+        c.k = at(a.KV, (int64_t)l * 2 * dd), c.k_ld = kvld, c.k_bs = (int64_t)N * kvld;
+        c.v = at(a.KV, (int64_t)l * 2 * dd + dd), c.v_ld = kvld, c.v_bs = (int64_t)N * kvld;
+        c.o_ld = (int64_t)Bimg * dd, c.o_bs = dd;
+        c.key_valid = a.valid, c.kv_bs = N;
+        c.temperature = std::sqrt((float)dkd);
+        c.prio = prio(s);
+        qa.cross = 1;
+        qa.X = reinterpret_cast<const bf16*>(g.x1), qa.ldx = (int64_t)Bimg * dd, qa.x_bs = dd;
+        qa.W = reinterpret_cast<const bf16*>(W(w.Wq_c)), qa.ldw = dd, qa.d = dd;
+        qa.qkv = nullptr, qa.ldqkv = dd, qa.o = reinterpret_cast<bf16*>(g.att);
+        require(qkv_attn_ok(qa), "internal: decode cross attention geometry");
+        if (stamp_on) c.stamp = stamp(s, "qkv_attn cross decode " + std::to_string(kb) + "x" + std::to_string(N));
+        qkv_attn_fwd(qa, s);
+      } else {
+        linear(g.x1, dd, w.Wq_c, dd, g.q, dd, act, R, dd, dd, nullptr, 0, s);
+        AttnGeom c;
+        c.B = R, c.H = Hd, c.Lq = 1, c.Lk = N, c.dk = dkd;
+        c.q = g.q, c.q_ld = dd, c.q_bs = dd;
+        c.k = at(a.KV, (int64_t)l * 2 * dd), c.k_ld = kvld, c.k_bs = (int64_t)N * kvld;
+        c.v = at(a.KV, (int64_t)l * 2 * dd + dd), c.v_ld = kvld, c.v_bs = (int64_t)N * kvld;
+        c.kv_bmod = Bimg;
+        c.o_ld = dd, c.o_bs = dd;
+        c.key_valid = a.valid, c.kv_bs = N;
+        c.temperature = std::sqrt((float)dkd);
+        attf(c, g.att, want_p ? g.Pc : nullptr, act, s);
+      }
       linear(g.att, dd, w.Wo_c, dd, g.tmp, dd, act, R, dd, dd, nullptr, 0, s);
       LnFwd l2;
       l2.M = R, l2.d = dd, l2.a = g.tmp, l2.res = g.x1, l2.gamma = P(w.lcg), l2.beta = P(w.lcb), l2.y = g.x2;

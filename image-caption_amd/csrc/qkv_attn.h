@@ -9,12 +9,14 @@ namespace capgen {
 // are what the backward reads); g.Lq == g.Lk == rows per image.
 struct QkvAttn {
   AttnGeom g;
-  const bf16* X = nullptr;  // [B * L][ldx]
+  const bf16* X = nullptr;  // row r of image b at X + b * x_bs + r * ldx
   int64_t ldx = 0;
+  int64_t x_bs = -1;        // -1: L * ldx (images' rows contiguous); beam decode: the rows of image b
+                            // are r = j * B + b, so ldx = B * d and x_bs = d
   const bf16* W = nullptr;  // Wqkv [3d][ldw] (nn.Linear layout)
   int64_t ldw = 0;
   int d = 0;
-  bf16* qkv = nullptr;  // [B * L][ldqkv]: q | k | v
+  bf16* qkv = nullptr;  // [B * L][ldqkv]: q | k | v (null: not stored, decode)
   int64_t ldqkv = 0;
   bf16* o = nullptr;  // attention output, g.o_ld / g.o_bs
   // cross attention (DecoderBlock's second MHA, modules.py:195-197): only q = X . Wq^T is projected

@@ -50,7 +50,7 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   constexpr int NF = NP;  // 16-column fragments per wave (48 or 16 of the 64 NP columns)
   const int L = g.Lq;     // rows of X (query rows)
-  const bf16* xb = a.X + (int64_t)b * L * a.ldx;
+  const bf16* xb = a.X + (int64_t)b * (a.x_bs >= 0 ? a.x_bs : (int64_t)L * a.ldx);
 
   // ---- first weight batch, X rows (clamped row, unconditional: no load waits at a branch join),
   // key flags; then the LDS writes: X (rows >= L zero), zeroed attention images.
@@ -153,7 +153,7 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
 
   // ---- bf16 results -> the qkv buffer (backward) and the LDS images (attention) ----
   // lane holds C[row 16i + fr][col 16 NF w + 16f + 4fg + 0..3]
-  bf16* qkvb = a.qkv + (int64_t)b * L * a.ldqkv;
+  bf16* qkvb = a.qkv ? a.qkv + (int64_t)b * L * a.ldqkv : nullptr;
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
     const int c = 16 * NF * w + 16 * f + 4 * fg, which = c >> 6, within = c & 63;
@@ -164,7 +164,7 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
       const f32x4 v = acc[i][f];
       const bf16x4 r4 = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
       if (row < L) {
-        *reinterpret_cast<bf16x4*>(qkvb + (int64_t)row * a.ldqkv + which * QD + h * DK + within) = r4;
+        if (a.qkv) *reinterpret_cast<bf16x4*>(qkvb + (int64_t)row * a.ldqkv + which * QD + h * DK + within) = r4;
         *reinterpret_cast<bf16x4*>(img + row * 128 + swz(row, within >> 3) * 16 + (within & 7) * 2) = r4;
       }
     }
@@ -191,7 +191,8 @@ void qkv_attn_fwd(const QkvAttn& a, hipStream_t s) {
     using namespace hz;
     const int L = g.Lq;
     const int np = a.cross ? 1 : 3, Bk = g.kv_bmod > 0 ? std::min(g.B, g.kv_bmod) : g.B;
-    const Rgn r[] = {rows_blk(a.X, g.B, L, (int64_t)L * a.ldx, a.ldx, a.d, 2, RD), rd(a.W, (int64_t)np * a.d * a.ldw * 2),
+    const Rgn r[] = {rows_blk(a.X, g.B, L, a.x_bs >= 0 ? a.x_bs : (int64_t)L * a.ldx, a.ldx, a.d, 2, RD),
+                     rd(a.W, (int64_t)np * a.d * a.ldw * 2),
                      blk(g.key_valid, Bk, g.Lk, g.kv_bs, RD), blk(g.key_ids, g.B, (int64_t)g.Lk * 4, g.kid_bs * 4, RD),
                      rows_blk(a.cross ? g.k : nullptr, Bk, g.Lk, g.k_bs, g.k_ld, a.d, 2, RD),
                      rows_blk(a.cross ? g.v : nullptr, Bk, g.Lk, g.v_bs, g.v_ld, a.d, 2, RD),

@@ -1579,6 +1579,7 @@ def test_grouped_decode_attention_lds_staging_bit_identical(monkeypatch):
     """bf16 beam decode at C4 (B=256, beam 5): the grouped cross-attention with the image's K/V
     staged in LDS once per (image, head) workgroup (CAPGEN_DECODE_GROUP_LDS, default) gives the same
     beam ids as the per-wave register loads (same per-lane values, same sums)."""
+    monkeypatch.setenv("CAPGEN_FUSED_QKV", "0")  # (the fused cross front bypasses the grouped kernel)
     _, cfg, sd, e, f, p, c = _c2_setup(B=256, dtype="bf16", weights="fixture")
     e.set_training(False)
     fd, pd = f.to(DEV).bfloat16(), p.to(DEV)
@@ -1588,3 +1589,32 @@ def test_grouped_decode_attention_lds_staging_bit_identical(monkeypatch):
     b = e.beam(fd, pd, 5).clone()
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+def test_fused_attention_fronts_track_separate_launches_bf16(monkeypatch):
+    """The fused self / cross attention fronts (qkv_attn.hip; CAPGEN_FUSED_QKV, default on) against the
+    GEMM + attention launches they replace, on bench.py's C2 step and C4-style decode (bf16, fixture
+    weights): the projections differ only by summation order (last-bit roundings), so the loss agrees
+    to 1e-3, every gradient to 2 % relative L2, and at least 97 % of the greedy / beam-5 decodes are
+    identical (the rest are near-ties)."""
+    monkeypatch.setenv("CAPGEN_FUSED_QKV", "0")
+    _, cfg, sd, e0, f, p, c = _c2_setup(dtype="bf16", weights="fixture")
+    monkeypatch.delenv("CAPGEN_FUSED_QKV")
+    _, _, _, e1, _, _, _ = _c2_setup(dtype="bf16", weights="fixture")
+    fd, pd, cd = f.to(DEV).bfloat16(), p.to(DEV), c.to(DEV)
+    for e in (e0, e1):
+        e.set_training(False)
+    l0, l1 = e0.forward(fd, pd, cd).item(), e1.forward(fd, pd, cd).item()
+    assert abs(l0 - l1) <= 1e-3 * abs(l0), (l0, l1)
+    e0.backward()
+    e1.backward()
+    g0, g1 = e0.grads_state_dict(), e1.grads_state_dict()
+    worst = max((((g1[n].double() - g0[n].double()).norm() / (g0[n].double().norm() + 1e-12)).item(), n) for n in g0)
+    assert worst[0] < 2e-2, worst
+    ids0, _ = e0.greedy(fd, pd)
+    ids1, _ = e1.greedy(fd, pd)
+    same = (ids0 == ids1).all(1).float().mean().item()
+    assert same >= 0.97, same
+    b0, b1 = e0.beam(fd, pd, 5), e1.beam(fd, pd, 5)
+    same = (b0 == b1).all(1).float().mean().item()
+    assert same >= 0.97, same
