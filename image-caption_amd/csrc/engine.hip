@@ -1753,6 +1753,18 @@ struct capgen_engine {
     for (int l = 0; l < L.Ld; ++l) {
       const auto& w = L.dec[l];
       void* cl = at(cache, (int64_t)l * R * cld);
+      QkvDecode qd;
+      qd.B = Bimg, qd.H = Hd, qd.kb = R / Bimg, qd.t = t, qd.d = dd, qd.prio = prio(s);
+      qd.X = reinterpret_cast<const bf16*>(g.x), qd.W = reinterpret_cast<const bf16*>(W(w.Wqkv));
+      qd.cache = reinterpret_cast<bf16*>(cl), qd.c_ld = cld, qd.kv_row = kv_row, qd.kv_row_ld = Tc;
+      qd.ids = ids, qd.ids_ld = Tc, qd.pad_idx = cfg.pad_idx, qd.temperature = std::sqrt((float)dkd);
+      qd.o = reinterpret_cast<bf16*>(g.att);
+      if (act == DType::BF16 && fused_qkv_on && R % Bimg == 0 && qkv_decode_ok(qd)) {
+        // the step's Q/K/V projection, the cache write and the self attention in one launch
+        // (qkv_attn.hip qkv_decode_kernel, one workgroup per (image, head))
+        if (stamp_on) qd.stamp = stamp(s, "qkv_decode self " + std::to_string(qd.kb) + "x" + std::to_string(t + 1));
+        qkv_decode_self(qd, s);
+      } else {
       if (act == DType::BF16) {  // one GEMM: Q columns -> g.q, K/V columns -> the cache at position t
         GemmArgs ga;
         ga.M = R, ga.N = 3 * dd, ga.K = dd, ga.A = g.x, ga.lda = dd, ga.B = W(w.Wqkv), ga.ldb = dd;
@@ -1773,6 +1785,7 @@ struct capgen_engine {
       sg.kv_row = kv_row, sg.kv_row_ld = Tc;
       sg.temperature = std::sqrt((float)dkd);
       attf(sg, g.att, nullptr, act, s);
+      }
       linear(g.att, dd, w.Wo_s, dd, g.tmp, dd, act, R, dd, dd, nullptr, 0, s);
       LnFwd l1;
       l1.M = R, l1.d = dd, l1.a = g.tmp, l1.res = g.x, l1.gamma = P(w.lsg), l1.beta = P(w.lsb), l1.y = g.x1;

@@ -1594,27 +1594,35 @@ def test_grouped_decode_attention_lds_staging_bit_identical(monkeypatch):
 def test_fused_attention_fronts_track_separate_launches_bf16(monkeypatch):
     """The fused self / cross attention fronts (qkv_attn.hip; CAPGEN_FUSED_QKV, default on) against the
     GEMM + attention launches they replace, on bench.py's C2 step and C4-style decode (bf16, fixture
-    weights): the projections differ only by summation order (last-bit roundings), so the loss agrees
-    to 1e-3, every gradient to 2 % relative L2, and at least 97 % of the greedy / beam-5 decodes are
-    identical (the rest are near-ties)."""
+    weights).  The projections differ only by summation order (last-bit roundings), so: the losses
+    agree to 1e-3; measured against the fp32 parity engine, no gradient of the fused engine is further
+    off than 1.5x the separate-launch engine's own bf16 error (+1 % of the tensor), and none beyond the
+    10 % of test_c2_full_size_bf16_train_mode_close_to_fp32; at least 97 % of the greedy / beam-5
+    decodes are identical (the rest are near-ties)."""
     monkeypatch.setenv("CAPGEN_FUSED_QKV", "0")
     _, cfg, sd, e0, f, p, c = _c2_setup(dtype="bf16", weights="fixture")
     monkeypatch.delenv("CAPGEN_FUSED_QKV")
     _, _, _, e1, _, _, _ = _c2_setup(dtype="bf16", weights="fixture")
-    fd, pd, cd = f.to(DEV).bfloat16(), p.to(DEV), c.to(DEV)
-    for e in (e0, e1):
+    _, _, _, e32, _, _, _ = _c2_setup(dtype="fp32", weights="fixture")
+    fd, pd, cd = f.to(DEV), p.to(DEV), c.to(DEV)
+    for e in (e0, e1, e32):
         e.set_training(False)
-    l0, l1 = e0.forward(fd, pd, cd).item(), e1.forward(fd, pd, cd).item()
+    l0, l1 = e0.forward(fd.bfloat16(), pd, cd).item(), e1.forward(fd.bfloat16(), pd, cd).item()
+    e32.forward(fd, pd, cd)
     assert abs(l0 - l1) <= 1e-3 * abs(l0), (l0, l1)
-    e0.backward()
-    e1.backward()
-    g0, g1 = e0.grads_state_dict(), e1.grads_state_dict()
-    worst = max((((g1[n].double() - g0[n].double()).norm() / (g0[n].double().norm() + 1e-12)).item(), n) for n in g0)
-    assert worst[0] < 2e-2, worst
-    ids0, _ = e0.greedy(fd, pd)
-    ids1, _ = e1.greedy(fd, pd)
+    for e in (e0, e1, e32):
+        e.backward()
+    g0, g1, g32 = e0.grads_state_dict(), e1.grads_state_dict(), e32.grads_state_dict()
+    for n in g32:
+        ref = g32[n].double()
+        rel = lambda g: ((g.double() - ref).norm() / (ref.norm() + 1e-12)).item()
+        r0, r1 = rel(g0[n]), rel(g1[n])
+        assert r1 <= 1.5 * r0 + 1e-2 and r1 < 0.1, (n, r1, r0)
+    fb = fd.bfloat16()
+    ids0, _ = e0.greedy(fb, pd)
+    ids1, _ = e1.greedy(fb, pd)
     same = (ids0 == ids1).all(1).float().mean().item()
     assert same >= 0.97, same
-    b0, b1 = e0.beam(fd, pd, 5), e1.beam(fd, pd, 5)
+    b0, b1 = e0.beam(fb, pd, 5), e1.beam(fb, pd, 5)
     same = (b0 == b1).all(1).float().mean().item()
     assert same >= 0.97, same
