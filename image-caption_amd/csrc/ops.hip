@@ -662,25 +662,27 @@ __global__ void __launch_bounds__(256) ce_finish_kernel(const float2* __restrict
   typedef __attribute__((ext_vector_type(4))) __bf16 b4;
   const int m = blockIdx.x, nsl = (V + 15) / 16;
   bf16* row = dl + (int64_t)m * V;
+  // every load first -- target, target logit, slab stats, the row's e values -- from clamped in-range
+  // addresses with no branch around them (a load in a branch is waited for at its join): one round trip
   const int y = tgt[m];
-  if (y == pad) {
-    for (int c = threadIdx.x * 4; c < V; c += 256 * 4) *reinterpret_cast<b4*>(row + c) = b4{0, 0, 0, 0};
-    if (threadIdx.x == 0) loss_row[m] = 0.f;
-    return;
-  }
+  const float tl = tlogit[m];
   float2 st[SPT];
   b4 e[SPT][4];
 #pragma unroll
   for (int u = 0; u < SPT; ++u) {
-    const int c = threadIdx.x + 256 * u;
-    st[u] = c < nsl ? stats[(int64_t)m * ld + c] : float2{-INFINITY, 0.f};
+    const int c = threadIdx.x + 256 * u, cc = min(c, nsl - 1);
+    st[u] = stats[(int64_t)m * ld + cc];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int col = c * 16 + q * 4;
-      e[u][q] = c < nsl && col < V ? *reinterpret_cast<const b4*>(row + col) : b4{0, 0, 0, 0};
-    }
+    for (int q = 0; q < 4; ++q) e[u][q] = *reinterpret_cast<const b4*>(row + min(cc * 16 + q * 4, V - 4));
   }
-  const float tl = threadIdx.x == 0 ? tlogit[m] : 0.f;
+#pragma unroll
+  for (int u = 0; u < SPT; ++u)
+    if (threadIdx.x + 256 * u >= nsl) st[u] = float2{-INFINITY, 0.f};
+  if (y == pad) {  // (uniform per workgroup)
+    for (int c = threadIdx.x * 4; c < V; c += 256 * 4) *reinterpret_cast<b4*>(row + c) = b4{0, 0, 0, 0};
+    if (threadIdx.x == 0) loss_row[m] = 0.f;
+    return;
+  }
   float mx = -INFINITY;
 #pragma unroll
   for (int u = 0; u < SPT; ++u) mx = fmaxf(mx, st[u].x);
