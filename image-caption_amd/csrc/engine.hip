@@ -1753,18 +1753,6 @@ struct capgen_engine {
     for (int l = 0; l < L.Ld; ++l) {
       const auto& w = L.dec[l];
       void* cl = at(cache, (int64_t)l * R * cld);
-      QkvDecode qd;
-      qd.B = Bimg, qd.H = Hd, qd.kb = R / Bimg, qd.t = t, qd.d = dd, qd.prio = prio(s);
-      qd.X = reinterpret_cast<const bf16*>(g.x), qd.W = reinterpret_cast<const bf16*>(W(w.Wqkv));
-      qd.cache = reinterpret_cast<bf16*>(cl), qd.c_ld = cld, qd.kv_row = kv_row, qd.kv_row_ld = Tc;
-      qd.ids = ids, qd.ids_ld = Tc, qd.pad_idx = cfg.pad_idx, qd.temperature = std::sqrt((float)dkd);
-      qd.o = reinterpret_cast<bf16*>(g.att);
-      if (act == DType::BF16 && fused_qkv_on && R % Bimg == 0 && qkv_decode_ok(qd)) {
-        // the step's Q/K/V projection, the cache write and the self attention in one launch
-        // (qkv_attn.hip qkv_decode_kernel, one workgroup per (image, head))
-        if (stamp_on) qd.stamp = stamp(s, "qkv_decode self " + std::to_string(qd.kb) + "x" + std::to_string(t + 1));
-        qkv_decode_self(qd, s);
-      } else {
       if (act == DType::BF16) {  // one GEMM: Q columns -> g.q, K/V columns -> the cache at position t
         GemmArgs ga;
         ga.M = R, ga.N = 3 * dd, ga.K = dd, ga.A = g.x, ga.lda = dd, ga.B = W(w.Wqkv), ga.ldb = dd;
@@ -1785,46 +1773,22 @@ struct capgen_engine {
       sg.kv_row = kv_row, sg.kv_row_ld = Tc;
       sg.temperature = std::sqrt((float)dkd);
       attf(sg, g.att, nullptr, act, s);
-      }
       linear(g.att, dd, w.Wo_s, dd, g.tmp, dd, act, R, dd, dd, nullptr, 0, s);
       LnFwd l1;
       l1.M = R, l1.d = dd, l1.a = g.tmp, l1.res = g.x, l1.gamma = P(w.lsg), l1.beta = P(w.lsb), l1.y = g.x1;
       lnf(l1, s);
       const bool want_p = want_attn && l == L.Ld - 1;
-      const int kb = R / Bimg;  // rows per image (beams): row r = j * Bimg + image
-      if (!want_p && R % Bimg == 0 && cross_fusable(kb)) {
-        // the query projection and the cross attention of every image's kb rows in one launch
-        // (qkv_attn.hip cross mode, one workgroup per (image, head); the query is not stored)
-        QkvAttn qa;
-        AttnGeom& c = qa.g;
-        c.B = Bimg, c.H = Hd, c.Lq = kb, c.Lk = N, c.dk = dkd;
-        c.q = g.q, c.q_ld = (int64_t)Bimg * dd, c.q_bs = dd;
-        c.k = at(a.KV, (int64_t)l * 2 * dd), c.k_ld = kvld, c.k_bs = (int64_t)N * kvld;
-        c.v = at(a.KV, (int64_t)l * 2 * dd + dd), c.v_ld = kvld, c.v_bs = (int64_t)N * kvld;
-        c.o_ld = (int64_t)Bimg * dd, c.o_bs = dd;
-        c.key_valid = a.valid, c.kv_bs = N;
-        c.temperature = std::sqrt((float)dkd);
-        c.prio = prio(s);
-        qa.cross = 1;
-        qa.X = reinterpret_cast<const bf16*>(g.x1), qa.ldx = (int64_t)Bimg * dd, qa.x_bs = dd;
-        qa.W = reinterpret_cast<const bf16*>(W(w.Wq_c)), qa.ldw = dd, qa.d = dd;
-        qa.qkv = nullptr, qa.ldqkv = dd, qa.o = reinterpret_cast<bf16*>(g.att);
-        require(qkv_attn_ok(qa), "internal: decode cross attention geometry");
-        if (stamp_on) c.stamp = stamp(s, "qkv_attn cross decode " + std::to_string(kb) + "x" + std::to_string(N));
-        qkv_attn_fwd(qa, s);
-      } else {
-        linear(g.x1, dd, w.Wq_c, dd, g.q, dd, act, R, dd, dd, nullptr, 0, s);
-        AttnGeom c;
-        c.B = R, c.H = Hd, c.Lq = 1, c.Lk = N, c.dk = dkd;
-        c.q = g.q, c.q_ld = dd, c.q_bs = dd;
-        c.k = at(a.KV, (int64_t)l * 2 * dd), c.k_ld = kvld, c.k_bs = (int64_t)N * kvld;
-        c.v = at(a.KV, (int64_t)l * 2 * dd + dd), c.v_ld = kvld, c.v_bs = (int64_t)N * kvld;
-        c.kv_bmod = Bimg;
-        c.o_ld = dd, c.o_bs = dd;
-        c.key_valid = a.valid, c.kv_bs = N;
-        c.temperature = std::sqrt((float)dkd);
-        attf(c, g.att, want_p ? g.Pc : nullptr, act, s);
-      }
+      linear(g.x1, dd, w.Wq_c, dd, g.q, dd, act, R, dd, dd, nullptr, 0, s);
+      AttnGeom c;  // rows r -> image r % Bimg
+      c.B = R, c.H = Hd, c.Lq = 1, c.Lk = N, c.dk = dkd;
+      c.q = g.q, c.q_ld = dd, c.q_bs = dd;
+      c.k = at(a.KV, (int64_t)l * 2 * dd), c.k_ld = kvld, c.k_bs = (int64_t)N * kvld;
+      c.v = at(a.KV, (int64_t)l * 2 * dd + dd), c.v_ld = kvld, c.v_bs = (int64_t)N * kvld;
+      c.kv_bmod = Bimg;
+      c.o_ld = dd, c.o_bs = dd;
+      c.key_valid = a.valid, c.kv_bs = N;
+      c.temperature = std::sqrt((float)dkd);
+      attf(c, g.att, want_p ? g.Pc : nullptr, act, s);
       linear(g.att, dd, w.Wo_c, dd, g.tmp, dd, act, R, dd, dd, nullptr, 0, s);
       LnFwd l2;
       l2.M = R, l2.d = dd, l2.a = g.tmp, l2.res = g.x1, l2.gamma = P(w.lcg), l2.beta = P(w.lcb), l2.y = g.x2;

@@ -59,7 +59,7 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   constexpr int NF = NP;  // 16-column fragments per wave (48 or 16 of the 64 NP columns)
   const int L = g.Lq;     // rows of X (query rows)
-  const bf16* xb = a.X + (int64_t)b * (a.x_bs >= 0 ? a.x_bs : (int64_t)L * a.ldx);
+  const bf16* xb = a.X + (int64_t)b * L * a.ldx;
 
   // ---- first weight batch, X rows (clamped row, unconditional: no load waits at a branch join),
   // key flags; then the LDS writes: X (rows >= L zero), zeroed attention images.
@@ -185,167 +185,6 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
   attn_fwd_staged(g, a.o, nullptr, b, h, sm);
 }
 
-// ---- KV-cached decode step, self attention (QkvDecode) ----
-// Phase 1 as qkv_attn_kernel<1, 3> (rows r = j * B + image, j < kb <= 16): the image's rows of x in
-// LDS, wave w projects 48 of the head's 192 columns.  The bf16 q / k / v go to LDS; k / v also to
-// every row's cache slot at position t.  Phase 2 as attn_decode_bf16_kernel's single mode (lane =
-// (key slot jr = lane / 8, 16-B chunk c = lane % 8), the 8-chunk dot, softmax and P.V reduced across
-// lanes with the same DPP / shuffle order): wave w runs rows j = w, w + 4, ...; key p < t from cache
-// row kv_row[r][p], key t from the LDS copy of the fresh k / v.
-template <int NIT>  // key slots of 8: t + 1 <= 8 NIT
-__global__ void __launch_bounds__(256) qkv_decode_kernel(QkvDecode a) {
-  __shared__ __attribute__((aligned(16))) char xs[16 * QD * 2];
-  __shared__ __attribute__((aligned(16))) bf16 qkv_s[3][16][DK];
-  StampScope stamp_scope(a.stamp);
-  if (a.prio) __builtin_amdgcn_s_setprio(3);
-  const int img = blockIdx.x / a.H, h = blockIdx.x % a.H;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int kb = a.kb, t = a.t;
-  const int64_t rstride = (int64_t)a.B * QD;  // x / o row of beam j: + j * B * d
-  const bf16* xb = a.X + (int64_t)img * QD;
-  const int fr = lane & 15, fg = lane >> 4;
-  const bf16* wrow[3];
-#pragma unroll
-  for (int f = 0; f < 3; ++f) {
-    const int c = 48 * w + 16 * f + fr, which = c >> 6, within = c & 63;
-    wrow[f] = a.W + (int64_t)(which * QD + h * DK + within) * QD + 8 * fg;
-  }
-  bf16x8 bq[2][QKB][3];
-#pragma unroll
-  for (int kk = 0; kk < QKB; ++kk)
-#pragma unroll
-    for (int f = 0; f < 3; ++f) bq[0][kk][f] = *reinterpret_cast<const bf16x8*>(wrow[f] + 32 * kk);
-  {
-    constexpr int PER = 16 * QD / 8 / 256;
-    uint4 v[PER];
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int c = tid + 256 * u, row = c / (QD / 8), ch = c % (QD / 8);
-      v[u] = *reinterpret_cast<const uint4*>(xb + (int64_t)min(row, kb - 1) * rstride + ch * 8);
-    }
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int c = tid + 256 * u, row = c / (QD / 8), ch = c % (QD / 8);
-      *reinterpret_cast<uint4*>(xs + row * (QD * 2) + xswz(row, ch) * 16) = row < kb ? v[u] : uint4{0u, 0u, 0u, 0u};
-    }
-  }
-  f32x4 acc[3];
-#pragma unroll
-  for (int f = 0; f < 3; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-  __syncthreads();
-#pragma unroll
-  for (int grp = 0; grp < QKS / QKB; ++grp) {
-    const int cur = grp & 1;
-    if (grp + 1 < QKS / QKB) {
-#pragma unroll
-      for (int kk = 0; kk < QKB; ++kk)
-#pragma unroll
-        for (int f = 0; f < 3; ++f)
-          bq[cur ^ 1][kk][f] = *reinterpret_cast<const bf16x8*>(wrow[f] + 32 * ((grp + 1) * QKB + kk));
-    }
-    __builtin_amdgcn_sched_barrier(0);  // (as in qkv_attn_kernel)
-#pragma unroll
-    for (int kk = 0; kk < QKB; ++kk) {
-      const int ks = grp * QKB + kk;
-      const bf16x8 af = *reinterpret_cast<const bf16x8*>(xs + fr * (QD * 2) + xswz(fr, 4 * ks + fg) * 16);
-#pragma unroll
-      for (int f = 0; f < 3; ++f) acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[cur][kk][f], af, acc[f], 0, 0, 0);
-    }
-  }
-  // lane holds [row fr][col 48w + 16f + 4fg + 0..3]: bf16 -> LDS (q, k, v) and k / v -> the cache
-#pragma unroll
-  for (int f = 0; f < 3; ++f) {
-    const int c = 48 * w + 16 * f + 4 * fg, which = c >> 6, within = c & 63;
-    const f32x4 v = acc[f];
-    const bf16x4 r4 = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-    if (fr < kb) {
-      *reinterpret_cast<bf16x4*>(&qkv_s[which][fr][within]) = r4;
-      if (which > 0) {
-        const int64_t r = (int64_t)fr * a.B + img;
-        *reinterpret_cast<bf16x4*>(a.cache + r * a.c_ld + (int64_t)t * 2 * QD + (which - 1) * QD + h * DK + within) = r4;
-      }
-    }
-  }
-  __syncthreads();
-  // ---- phase 2: one row per wave at a time ----
-  const int jr = lane >> 3, c = lane & 7;
-  const float inv_t = 1.f / a.temperature;
-  for (int j = w; j < kb; j += 4) {
-    const int64_t r = (int64_t)j * a.B + img;
-    // key slot p = jr + 8 it: its cache row (the beam it descends from), loaded up front
-    uint4 kr[NIT], vr[NIT];
-    bool kin[NIT];
-    int idp[NIT];
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int p = jr + 8 * it;
-      kin[it] = p <= t;
-      const int pc = min(p, t);
-      const int64_t src = a.kv_row ? a.kv_row[r * a.kv_row_ld + pc] : r;
-      const bf16* kp = a.cache + src * a.c_ld + (int64_t)pc * 2 * QD + h * DK + c * 8;
-      kr[it] = *reinterpret_cast<const uint4*>(kp);
-      vr[it] = *reinterpret_cast<const uint4*>(kp + QD);
-      idp[it] = a.ids[r * a.ids_ld + pc];
-    }
-#pragma unroll
-    for (int it = 0; it < NIT; ++it)
-      if (jr + 8 * it == t) {  // position t: this row's fresh k / v (LDS, not the just-written cache)
-        kr[it] = *reinterpret_cast<const uint4*>(&qkv_s[1][j][c * 8]);
-        vr[it] = *reinterpret_cast<const uint4*>(&qkv_s[2][j][c * 8]);
-      }
-    float q[8];
-    bf8_to_f(*reinterpret_cast<const uint4*>(&qkv_s[0][j][c * 8]), q);
-    float sc[NIT];
-    float mx = -INFINITY;
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      float k[8];
-      bf8_to_f(kr[it], k);
-      float dot = 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dot = fmaf(q[e] * inv_t, k[e], dot);
-      dot += dpp_f<kDppXor1>(dot);
-      dot += dpp_f<kDppXor2>(dot);
-      dot += dpp_f<kDppHalfMirror>(dot);
-      sc[it] = kin[it] && idp[it] != a.pad_idx ? dot : -INFINITY;
-      mx = fmaxf(mx, sc[it]);
-    }
-    mx = fmaxf(mx, dpp_f<kDppRor8>(mx));
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    float sum = 0.f;
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      sc[it] = kin[it] ? expf(sc[it] - mx) : 0.f;
-      sum += sc[it];
-    }
-    sum += dpp_f<kDppRor8>(sum);
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
-    const float inv = 1.f / sum;
-    float ov[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const float pr = sc[it] * inv;
-      float v[8];
-      bf8_to_f(vr[it], v);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) ov[e] = fmaf(pr, v[e], ov[e]);
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      ov[e] += dpp_f<kDppRor8>(ov[e]);
-      ov[e] += __shfl_xor(ov[e], 16, 64);
-      ov[e] += __shfl_xor(ov[e], 32, 64);
-    }
-    if (jr == 0) {
-      const bf16x8 ob = {(bf16)ov[0], (bf16)ov[1], (bf16)ov[2], (bf16)ov[3], (bf16)ov[4], (bf16)ov[5], (bf16)ov[6], (bf16)ov[7]};
-      *reinterpret_cast<bf16x8*>(a.o + r * QD + h * DK + c * 8) = ob;
-    }
-  }
-}
-
 }  // namespace
 
 bool qkv_attn_ok(const QkvAttn& a) {
@@ -364,7 +203,7 @@ void qkv_attn_fwd(const QkvAttn& a, hipStream_t s) {
     using namespace hz;
     const int L = g.Lq;
     const int np = a.cross ? 1 : 3, Bk = g.kv_bmod > 0 ? std::min(g.B, g.kv_bmod) : g.B;
-    const Rgn r[] = {rows_blk(a.X, g.B, L, a.x_bs >= 0 ? a.x_bs : (int64_t)L * a.ldx, a.ldx, a.d, 2, RD),
+    const Rgn r[] = {rows_blk(a.X, g.B, L, (int64_t)L * a.ldx, a.ldx, a.d, 2, RD),
                      rd(a.W, (int64_t)np * a.d * a.ldw * 2),
                      blk(g.key_valid, Bk, g.Lk, g.kv_bs, RD), blk(g.key_ids, g.B, (int64_t)g.Lk * 4, g.kid_bs * 4, RD),
                      rows_blk(a.cross ? g.k : nullptr, Bk, g.Lk, g.k_bs, g.k_ld, a.d, 2, RD),
@@ -390,32 +229,6 @@ void qkv_attn_fwd(const QkvAttn& a, hipStream_t s) {
       default: qkv_attn_kernel<4, 3><<<grid, 256, 0, s>>>(a); break;
     }
   }
-  CAPGEN_HIP(hipGetLastError());
-}
-
-}  // namespace capgen
-
-namespace capgen {
-
-bool qkv_decode_ok(const QkvDecode& a) {
-  return a.d == QD && a.H * DK == QD && a.kb >= 1 && a.kb <= 16 && a.t >= 0 && a.t < 64 && a.ids && a.c_ld % 8 == 0;
-}
-
-void qkv_decode_self(const QkvDecode& a, hipStream_t s) {
-  require(qkv_decode_ok(a), "qkv_decode_self: unsupported geometry (d = 512, head size 64, <= 16 rows per image, t < 64)");
-  if (hz::active()) {
-    using namespace hz;
-    const int64_t R = (int64_t)a.B * a.kb;
-    const Rgn r[] = {rd(a.X, R * a.d * 2), rd(a.W, (int64_t)3 * a.d * a.d * 2), rd(a.kv_row, R * a.kv_row_ld * 4),
-                     rd(a.ids, R * a.ids_ld * 4), blk(a.cache, R, (int64_t)(a.t + 1) * 2 * a.d * 2, a.c_ld * 2, ACC),
-                     wr(a.o, R * a.d * 2)};
-    op(s, "qkv_decode_self", r, sizeof r / sizeof r[0]);
-  }
-  const dim3 grid(a.B * a.H);
-  const int n = a.t + 1;
-  if (n <= 24) qkv_decode_kernel<3><<<grid, 256, 0, s>>>(a);
-  else if (n <= 40) qkv_decode_kernel<5><<<grid, 256, 0, s>>>(a);
-  else qkv_decode_kernel<8><<<grid, 256, 0, s>>>(a);
   CAPGEN_HIP(hipGetLastError());
 }
 
