@@ -397,6 +397,15 @@ __global__ void __launch_bounds__(512) attn_decode_bf16_kernel(AttnGeom g, int G
   const int Lk = g.Lk;
   const bf16* kb = reinterpret_cast<const bf16*>(g.k) + (int64_t)bk * g.k_bs + h * 64 + c * 8;
   const bf16* vb = reinterpret_cast<const bf16*>(g.v) + (int64_t)bk * g.v_bs + h * 64 + c * 8;
+  // the query chunk of query qi (clamped to a valid query: the prefetch past the last one is unused)
+  auto qload = [&](int qi) {
+    const int b = group ? min(qi, G - 1) * g.kv_bmod + b0 : b0;
+    return *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(g.q) + (int64_t)b * g.q_bs + h * 64 + c * 8);
+  };
+  // the first query is loaded with the K/V rows, each later one while the previous query computes
+  // (group mode: a wave runs up to 8 queries; a load at the top of each iteration was one more
+  // memory round trip per query)
+  uint4 qnext = qload(qfirst);
   // beam row table: lane l holds the cache row of key l (single mode only)
   const int rl = (!group && g.kv_row && lane < Lk) ? g.kv_row[(int64_t)b0 * g.kv_row_ld + lane] - bk : 0;
   uint4 kr[NIT], vr[NIT];
@@ -435,8 +444,8 @@ __global__ void __launch_bounds__(512) attn_decode_bf16_kernel(AttnGeom g, int G
   for (int qi = qfirst; qi < G; qi += qstep) {
     const int b = group ? qi * g.kv_bmod + b0 : b0;
     float q[8];
-    bf16x8_to_f(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(g.q) + (int64_t)b * g.q_bs + h * 64 + c * 8),
-                q);
+    bf16x8_to_f(qnext, q);
+    qnext = qload(qi + qstep);
     float s[NIT];
     float mx = -INFINITY;
 #pragma unroll
