@@ -1780,14 +1780,24 @@ struct capgen_engine {
       const bool want_p = want_attn && l == L.Ld - 1;
       linear(g.x1, dd, w.Wq_c, dd, g.q, dd, act, R, dd, dd, nullptr, 0, s);
       AttnGeom c;  // rows r -> image r % Bimg
-      c.B = R, c.H = Hd, c.Lq = 1, c.Lk = N, c.dk = dkd;
-      c.q = g.q, c.q_ld = dd, c.q_bs = dd;
+      c.H = Hd, c.Lk = N, c.dk = dkd;
       c.k = at(a.KV, (int64_t)l * 2 * dd), c.k_ld = kvld, c.k_bs = (int64_t)N * kvld;
       c.v = at(a.KV, (int64_t)l * 2 * dd + dd), c.v_ld = kvld, c.v_bs = (int64_t)N * kvld;
-      c.kv_bmod = Bimg;
-      c.o_ld = dd, c.o_bs = dd;
       c.key_valid = a.valid, c.kv_bs = N;
       c.temperature = std::sqrt((float)dkd);
+      const int kb = R / Bimg;  // beam rows per image: row j * Bimg + b
+      if (act == DType::BF16 && cross_mfma_on && !want_p && kb > 1 && R % Bimg == 0 && kb <= 64) {
+        // an image's kb beam rows as ONE query block of the MFMA attention (attention_mfma.hip), one
+        // workgroup per (image, head): the rows are Bimg * d apart
+        c.B = Bimg, c.Lq = kb;
+        c.q = g.q, c.q_ld = (int64_t)Bimg * dd, c.q_bs = dd;
+        c.o_ld = (int64_t)Bimg * dd, c.o_bs = dd;
+      } else {
+        c.B = R, c.Lq = 1;
+        c.q = g.q, c.q_ld = dd, c.q_bs = dd;
+        c.kv_bmod = Bimg;
+        c.o_ld = dd, c.o_bs = dd;
+      }
       attf(c, g.att, want_p ? g.Pc : nullptr, act, s);
       linear(g.att, dd, w.Wo_c, dd, g.tmp, dd, act, R, dd, dd, nullptr, 0, s);
       LnFwd l2;
@@ -1816,6 +1826,12 @@ struct capgen_engine {
       linear(xo, dd, L.Wc, dd, g.logits, L.V, DType::F32, R, L.V, dd, P(L.bc), 0, s);
     }
   }
+  // bf16 beam decode: the cross attention of an image's beam rows on the MFMA attention kernel
+  // (CAPGEN_DECODE_CROSS_MFMA=0: the grouped VALU decode kernel, attention.hip)
+  bool cross_mfma_on = [] {
+    const char* e = std::getenv("CAPGEN_DECODE_CROSS_MFMA");
+    return !(e && e[0] == '0');
+  }();
   // bf16 decode: the classifier epilogue writes slab stats and the greedy / beam selection reads
   // k * 16 logits per row instead of the whole row (CAPGEN_SLAB_DECODE=0: full-row kernels)
   bool slab_decode_on = [] {

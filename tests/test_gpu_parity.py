@@ -1579,6 +1579,7 @@ def test_grouped_decode_attention_lds_staging_bit_identical(monkeypatch):
     """bf16 beam decode at C4 (B=256, beam 5): the grouped cross-attention with the image's K/V
     staged in LDS once per (image, head) workgroup (CAPGEN_DECODE_GROUP_LDS, default) gives the same
     beam ids as the per-wave register loads (same per-lane values, same sums)."""
+    monkeypatch.setenv("CAPGEN_DECODE_CROSS_MFMA", "0")  # (the beam cross attention on the grouped kernel)
     _, cfg, sd, e, f, p, c = _c2_setup(B=256, dtype="bf16", weights="fixture")
     e.set_training(False)
     fd, pd = f.to(DEV).bfloat16(), p.to(DEV)
@@ -1590,19 +1591,21 @@ def test_grouped_decode_attention_lds_staging_bit_identical(monkeypatch):
     assert torch.equal(a, b)
 
 
-def test_fused_attention_fronts_track_separate_launches_bf16(monkeypatch):
+@pytest.mark.parametrize("knob", ["CAPGEN_FUSED_QKV", "CAPGEN_DECODE_CROSS_MFMA"])
+def test_fused_attention_fronts_track_separate_launches_bf16(monkeypatch, knob):
     """The fused self / cross attention fronts (qkv_attn.hip; CAPGEN_FUSED_QKV, default on) against the
-    GEMM + attention launches they replace, on bench.py's C2 step and C4-style decode (bf16, fixture
-    weights).  The projections differ only by summation order (last-bit roundings), so: the losses
+    GEMM + attention launches they replace, and the beam decode's cross attention on the MFMA attention
+    kernel (CAPGEN_DECODE_CROSS_MFMA, default on) against the grouped VALU decode kernel, on bench.py's
+    C2 step and C4-style decode (bf16, fixture weights).  The projections differ only by summation order (last-bit roundings), so: the losses
     agree to 1e-3; measured against the fp32 parity engine, no gradient of the fused engine is further
     off than 1.5x the separate-launch engine's own bf16 error (+1 % of the tensor), and none beyond the
     10 % of test_c2_full_size_bf16_train_mode_close_to_fp32; for greedy and beam-5 decodes, the fused
     engine's agreement with the fp32 engine's sequences is within 5 points of the separate engine's
     (beam search flips near-tied hypotheses on last-bit changes; measured 61/64 identical between the two
     bf16 engines on one run), and the two bf16 engines agree on at least 90 %."""
-    monkeypatch.setenv("CAPGEN_FUSED_QKV", "0")
+    monkeypatch.setenv(knob, "0")
     _, cfg, sd, e0, f, p, c = _c2_setup(dtype="bf16", weights="fixture")
-    monkeypatch.delenv("CAPGEN_FUSED_QKV")
+    monkeypatch.delenv(knob)
     _, _, _, e1, _, _, _ = _c2_setup(dtype="bf16", weights="fixture")
     _, _, _, e32, _, _, _ = _c2_setup(dtype="fp32", weights="fixture")
     fd, pd, cd = f.to(DEV), p.to(DEV), c.to(DEV)
