@@ -15,22 +15,34 @@ Me, Md = B * N, B * (T - 1)
 ENC = [(Me, 3 * d, d), (Me, d, d), (Me, f, d), (Me, d, f)] * 6
 DEC = [(Md, 3 * d, d), (Md, d, d), (Md, d, d), (Md, d, d), (Md, f, d), (Md, d, f)] * 6
 OTHER = [(Me, d, 2176), (Md, d, d), (Me, 12 * d, d), (Md, V, d)]
-FWD = ENC + DEC + OTHER
+# forward projections inside the fused attention fronts (qkv_attn_kernel, round 4): every self-attention
+# Q/K/V projection, and the cross-attention query projection of decoder blocks 1..5 (block 0's runs as a
+# GEMM on the side stream with the decoder front)
+FRONT = [(Me, 3 * d, d)] * 6 + [(Md, 3 * d, d)] * 6 + [(Md, d, d)] * 5
+FWD = [(Me, d, d), (Me, f, d), (Me, d, f)] * 6 + [(Md, d, d), (Md, d, d), (Md, f, d), (Md, d, f)] * 6 + \
+    [(Md, d, d)] + OTHER
 DX = ENC + DEC + OTHER[1:]
+FWD_ALL = ENC + DEC + OTHER
 LN_ROWS = [Me] * 13 + [Md] * 19
 ALG = {  # class -> (GFLOP, algorithmic GB) per step
     "GEMM fwd (NT)": (sum(2 * m * n * k for m, n, k in FWD) / 1e9,
                       sum((m * k + n * k) * 2 + m * n * 2 for m, n, k in FWD) / 1e9),
     "GEMM dX (NN)": (sum(2 * m * n * k for m, n, k in DX) / 1e9,
                      sum((m * n + n * k) * 2 + m * k * 2 for m, n, k in DX) / 1e9),
-    "GEMM dW (TN)": (sum(2 * m * n * k for m, n, k in FWD) / 1e9,
-                     sum((m * n + m * k) * 2 + n * k * 4 for m, n, k in FWD) / 1e9),
+    "GEMM dW (TN)": (sum(2 * m * n * k for m, n, k in FWD_ALL) / 1e9,
+                     sum((m * n + m * k) * 2 + n * k * 4 for m, n, k in FWD_ALL) / 1e9),
+    # fused front: read X, W, (cross: K/V); write the projection (kept for the backward) and o
+    "attention front (proj+attn)": (
+        sum(2 * m * n * k for m, n, k in FRONT) / 1e9,
+        (6 * (Me * d + 3 * d * d + Me * 3 * d + Me * d) + 6 * (Md * d + 3 * d * d + Md * 3 * d + Md * d)
+         + 5 * (Md * d + d * d + Md * d + 2 * Me * d + Md * d)) * 2 / 1e9),
     # y = LN(a + res): read a, res; write y, v (bf16)
     "LayerNorm fwd": (0, sum(4 * r * d * 2 for r in LN_ROWS) / 1e9),
     # read dy, v; write d_res, d_a
     "LayerNorm bwd": (0, sum(4 * r * d * 2 for r in LN_ROWS) / 1e9),
     # read q, k, v; write o  (self: rows x d each; cross: q/o over Md rows, k/v over Me rows)
-    "attention fwd": (0, (6 * 4 * Me * d * 2 + 6 * 4 * Md * d * 2 + 6 * (2 * Md + 2 * Me) * d * 2) / 1e9),
+    # (the one separate launch: decoder block 0's cross attention)
+    "attention fwd": (0, (2 * Md + 2 * Me) * d * 2 / 1e9),
     # read q, k, v, dO; write dq, dk, dv
     "attention bwd": (0, (6 * 7 * Me * d * 2 + 6 * 7 * Md * d * 2 + 6 * (3 * Md + 4 * Me) * d * 2) / 1e9),
     "Adam": (0, 30 * 55_707_408 / 1e9),
@@ -49,7 +61,7 @@ def klass(name):
             a = name.split("gemm_bf16_kernel<")[1].split(",")
             ta, tb = a[1].strip() == "true", a[2].strip() == "true"
         return "GEMM dW (TN)" if ta else "GEMM dX (NN)" if tb else "GEMM fwd (NT)"
-    for key, k in (("ln_fwd", "LayerNorm fwd"), ("ln_bwd", "LayerNorm bwd"), ("attn_fwd", "attention fwd"),
+    for key, k in (("qkv_attn", "attention front (proj+attn)"), ("ln_fwd", "LayerNorm fwd"), ("ln_bwd", "LayerNorm bwd"), ("attn_fwd", "attention fwd"),
                    ("attn_bwd", "attention bwd"), ("adam_kernel", "Adam"), ("ce_finish", "cross entropy"),
                    ("ce_reg", "cross entropy")):
         if key in name:
