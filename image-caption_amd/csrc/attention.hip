@@ -513,14 +513,10 @@ static void launch_decode(const AttnGeom& g, T* o, float* probs, hipStream_t s) 
     if (((g.q_bs | g.k_bs | g.v_bs | g.k_ld | g.v_ld | g.o_bs) % 8) == 0) {
       const int blocks = grouped ? g.kv_bmod * g.H : (g.B * g.H + 3) / 4;
       const int Gk = grouped ? G : 1;
-      // grouped: 2 waves share the image's queries (CAPGEN_DECODE_GROUP_WAVES = 1..8).  C4 beam 5,
-      // two alternating rounds per setting (round 3): 1 wave 14.7-15.7 ms/batch, 2 waves 14.2-14.5,
-      // 4 waves 14.6-14.7, 8 waves 15.1-15.2 (one wave per beam row, round 2: 25.1 vs 18.8 us/launch)
-      static const int gw_env = [] {
-        const char* e = std::getenv("CAPGEN_DECODE_GROUP_WAVES");
-        return e ? std::max(1, std::min(8, std::atoi(e))) : 2;
-      }();
-      const int nt = grouped ? 64 * gw_env : 256;
+      // grouped: 2 waves share the image's queries.  C4 beam 5, two alternating rounds per setting
+      // (round 3): 1 wave 14.7-15.7 ms/batch, 2 waves 14.2-14.5, 4 waves 14.6-14.7, 8 waves 15.1-15.2
+      // (one wave per beam row, round 2: 25.1 vs 18.8 us/launch)
+      const int nt = grouped ? 128 : 256;
       const char* kv_env = std::getenv("CAPGEN_DECODE_GROUP_LDS");  // (read per launch: tests toggle it)
       const int kv_lds = kv_env && kv_env[0] == '0' ? 0 : 1;
       const int lds = grouped ? kv_lds : 0;
@@ -559,14 +555,8 @@ __global__ void head_mean_kernel(const float* __restrict__ probs, int B, int H, 
   out[c] = acc / (float)H;
 }
 
-// CAPGEN_DECODE_GROUP=0: every decode row reads its image's K/V itself (A/B knob)
-static bool group_decode_on() {
-  static const bool on = [] {
-    const char* e = std::getenv("CAPGEN_DECODE_GROUP");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+// grouped decode (an image's beam rows in one workgroup, its K/V read once): always on
+static bool group_decode_on() { return true; }
 
 static void check_geom(const AttnGeom& g) {
   require(g.Lq >= 1 && g.Lq <= 64 && g.Lk >= 1 && g.Lk <= 64, "attention: Lq/Lk must be in [1, 64]");

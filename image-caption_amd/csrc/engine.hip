@@ -1125,12 +1125,9 @@ struct capgen_engine {
                 ns > 0 ? shadow + off : nullptr, (size_t)ns, s, grid_cap);
   }
   // Adam grid of the step's last buckets (embedding, encoder LN/biases), which sit between the
-  // backward's end and the next forward (CAPGEN_ADAM_TAIL_GRID; 0 = the common cap).  The whole
-  // chip for them measured slower (4-round A/B: 3.012 vs 2.982 ms/step with 2048 vs 256)
-  int tail_grid = [] {
-    const char* e = std::getenv("CAPGEN_ADAM_TAIL_GRID");
-    return e ? std::atoi(e) : 0;
-  }();
+  // backward's end and the next forward: the common cap (0).  The whole chip for them measured
+  // slower (4-round A/B: 3.012 vs 2.982 ms/step with 2048 vs 256 workgroups)
+  static constexpr int tail_grid = 0;
 
   // Step mode (train_step): the parameter update is bucketed.  A bucket is an arena range
   // whose gradients are final and whose weights nothing later in the backward pass reads
@@ -1272,12 +1269,8 @@ struct capgen_engine {
     const float p = cfg.dropout, pa = cfg.attention_dropout;
     // the striped LN/bias partials start at 0 (the critical stream's first LayerNorm backward adds
     // into them); the accumulated word-embedding gradient (20 MB at C2) is zeroed on es2 after the
-    // fork below -- its only writer is the embedding scatter on es2 (CAPGEN_EMB_MEMSET_SIDE=0: on s)
-    static const bool emb_side = [] {
-      const char* e = std::getenv("CAPGEN_EMB_MEMSET_SIDE");
-      return !(e && e[0] == '0');
-    }();
-    const bool emb_zero_side = emb_side && es2 != s && !L.has_img && !L.has_mf;
+    // fork below -- its only writer is the embedding scatter on es2
+    const bool emb_zero_side = es2 != s && !L.has_img && !L.has_mf;
     if (!emb_zero_side) memset_async(grads + L.n_dense, (L.enc_lng - L.n_dense) * sizeof(float), s);
     // the striped partials are cleared by the previous backward's folds (stripe_reduce(clear)); a
     // backward that did not reach both folds (diagnostic stops, errors) leaves them marked dirty

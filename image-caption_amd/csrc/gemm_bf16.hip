@@ -382,20 +382,8 @@ static Choice tune(const GemmArgs& g, hipStream_t s) {
     const char* e = std::getenv("CAPGEN_MAX_SPLITK");
     return e ? std::max(1, std::atoi(e)) : 8;
   }();
-  // diagnostic: CAPGEN_SPLITK_K=k1,k2,... allows split-K only for those K (bisecting a step)
-  static const std::vector<int> sk_only = [] {
-    std::vector<int> v;
-    if (const char* e = std::getenv("CAPGEN_SPLITK_K"))
-      for (const char* p = e; *p;) {
-        v.push_back(std::atoi(p));
-        while (*p && *p != ',') ++p;
-        if (*p) ++p;
-      }
-    return v;
-  }();
-  const bool sk_ok = sk_only.empty() || std::find(sk_only.begin(), sk_only.end(), g.K) != sk_only.end();
   for (int sk : {1, 2, 3, 4, 6, 8}) {
-    if (sk > max_sk || (sk > 1 && (nk < 4 * sk || !sk_ok))) break;
+    if (sk > max_sk || (sk > 1 && nk < 4 * sk)) break;
     if (sk > 1) ensure_ws(s, splitk_bytes(g, sk));
     for (int v = 1; v <= NVARIANTS; ++v) {
       if (!whole_lines<TO>(v) || (sk > 1 && kVariantKG[v] > 1)) continue;
@@ -585,11 +573,6 @@ static void launch_group(const GemmArgs* ps, int n, hipStream_t s) {
   std::vector<int> key{TA, TB, (int)sizeof(TO)};
   for (int i = 0; i < n; ++i) key.insert(key.end(), {ps[i].M, ps[i].N, ps[i].K});
   int v = g_variant % 100;
-  static const int forced = [] {  // experiment knob: every grouped launch on one variant
-    const char* e = std::getenv("CAPGEN_DWG_VARIANT");
-    return e ? std::atoi(e) : 0;
-  }();
-  if (v == 0 && forced) v = forced;
   if (v == 0) {
     std::lock_guard<std::mutex> lk(g_tune_mu);
     auto it = g_group_tuned.find(key);
