@@ -7,9 +7,10 @@ launches IN the step (capgen_debug_stamps: first workgroup start -> last workgro
 per candidate variant forced on every dX shape at once (CAPGEN_GEMM_FORCE, one child process per
 candidate), and picks per shape the variant with the smallest in-step time.
 
-  python tools/dx_incontention_tune.py            -> JSON lines: per candidate, per shape us; then
+  python tools/dx_incontention_tune.py [--fwd]    -> JSON lines: per candidate, per shape us; then
                                                      the choice per shape and the CAPGEN_GEMM_FORCE
-                                                     string that pins it
+                                                     string that pins it (--fwd: the NT forward
+                                                     GEMMs instead of the dX ones)
   python tools/dx_incontention_tune.py --worker   (child: one measurement, env set by the parent)
 """
 import json
@@ -23,6 +24,10 @@ sys.path.insert(0, os.path.join(REPO, "image-caption_amd"))
 # bf16-output variants (whole 128-B lines) without k-groups, + split-K forms for K = 2048
 CANDIDATES = [6, 7, 12, 13, 17, 20, 21, 4, 5, 8, 14, 15, 1, 3, 23, 24, 25, 26, 27, 28, 29, 30,
               206, 217, 221, 406, 417]
+
+
+FWD = "--fwd" in sys.argv
+CLASS, TA, TB = ("fwd", 0, 0) if FWD else ("dX", 0, 1)
 
 
 def worker():
@@ -61,7 +66,7 @@ def worker():
         torch.cuda.synchronize()
         for name, t0, t1 in eng.stamps(2):
             w = name.split()
-            if len(w) >= 4 and w[1] == "gemm" and w[2] == "dX" and t1 > t0 > 0:
+            if len(w) >= 4 and w[1] == "gemm" and w[2] == CLASS and t1 > t0 > 0:
                 s = shapes.setdefault(w[-1], [0, 0.0])
                 s[0] += 1
                 s[1] += t1 - t0
@@ -73,7 +78,8 @@ def worker():
 def run_child(env_extra):
     env = dict(os.environ)
     env.update(env_extra)
-    r = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), "--worker"], env=env, capture_output=True,
+    r = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), "--worker"] + (["--fwd"] if FWD else []),
+                       env=env, capture_output=True,
                        text=True, timeout=240)
     if r.returncode != 0:
         raise RuntimeError(f"worker failed ({r.returncode}): {r.stderr[-2000:]}")
@@ -86,7 +92,7 @@ def main():
     shapes = sorted(base["shapes"])  # "MxNxK" of the dX launches (layout NN: ta = 0, tb = 1)
     best = {s: ("tuned", base["shapes"][s][1]) for s in shapes}
     for v in CANDIDATES:
-        force = ";".join(f"{s.replace('x', ',')},0,1,{v}" for s in shapes
+        force = ";".join(f"{s.replace('x', ',')},{TA},{TB},{v}" for s in shapes
                          if v < 100 or int(s.split("x")[2]) >= 1024)
         if not force:
             continue
@@ -101,7 +107,7 @@ def main():
                 best[s] = (v, us)
     print(json.dumps({"choice": {s: {"variant": b[0], "us_per_step": b[1], "tuned_us": base["shapes"][s][1]}
                                  for s, b in best.items()}}), flush=True)
-    force = ";".join(f"{s.replace('x', ',')},0,1,{b[0]}" for s, b in best.items() if b[0] != "tuned")
+    force = ";".join(f"{s.replace('x', ',')},{TA},{TB},{b[0]}" for s, b in best.items() if b[0] != "tuned")
     print(json.dumps({"CAPGEN_GEMM_FORCE": force}), flush=True)
 
 
