@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <vector>
 
@@ -179,6 +180,32 @@ struct capgen_engine {
   hipEvent_t ev_ff = nullptr, ev_fj = nullptr;  // forward: decoder front forked to / joined from es2
   float *params = nullptr, *grads = nullptr, *am = nullptr, *av = nullptr;
   bf16* shadow = nullptr;
+  // the fused attention fronts' weights (every self-attention Wqkv, every cross Wq) in the tiled
+  // layout of qkv_tile_weights, re-tiled from the shadow wherever the shadow is written
+  bf16* wtile = nullptr;
+  std::map<int64_t, std::pair<int64_t, int>> tiled;  // arena offset -> (element offset in wtile, rows)
+  const bf16* WT(int64_t woff) const {
+    auto it = tiled.find(woff);
+    return it == tiled.end() ? nullptr : wtile + it->second.first;
+  }
+  void build_tiles() {  // (bf16 engines, at creation: model widths of 512 only)
+    std::vector<std::pair<int64_t, int>> ws;
+    if (L.d == 512) {
+      for (const auto& e : L.enc) ws.push_back({e.Wqkv, 3 * L.d});
+      if (L.has_img) ws.push_back({L.img.Wqkv, 3 * L.d});
+    }
+    if (L.dd == 512)
+      for (const auto& e : L.dec) ws.push_back({e.Wqkv, 3 * L.dd}), ws.push_back({e.Wq_c, L.dd});
+    int64_t n = 0;
+    for (auto& w : ws) tiled[w.first] = {n, w.second}, n += (int64_t)w.second * 512;
+    if (n) CAPGEN_HIP(hipMalloc(&wtile, (size_t)n * 2));
+  }
+  // re-tile the fronts' weights inside the arena range [off, off + n) from the shadow
+  void retile(int64_t off, int64_t n, hipStream_t s) {
+    for (auto& kv : tiled)
+      if (kv.first >= off && kv.first < off + n)
+        qkv_tile_weights(shadow + kv.first, kv.second.second, 512, wtile + kv.second.first, s);
+  }
   float* pe = nullptr;  // [max_length-1, dd] f32 sinusoid table
   int64_t* step = nullptr;
   float* adam_scal = nullptr;
@@ -403,7 +430,7 @@ struct capgen_engine {
     if (fused_qkv_on && act == DType::BF16 && !keep_probs(g)) {
       QkvAttn qa;
       qa.g = g, qa.g.prio = prio(s);
-      qa.X = reinterpret_cast<const bf16*>(X), qa.ldx = d, qa.W = reinterpret_cast<const bf16*>(W(wqkv)), qa.ldw = d;
+      qa.X = reinterpret_cast<const bf16*>(X), qa.ldx = d, qa.W = WT(wqkv);
       qa.d = d, qa.qkv = reinterpret_cast<bf16*>(qkv), qa.ldqkv = 3 * d, qa.o = reinterpret_cast<bf16*>(att);
       if (qkv_attn_ok(qa)) {
         if (stamp_on) qa.g.stamp = stamp(s, "qkv_attn " + std::to_string(g.Lq) + "x" + std::to_string(g.Lk));
@@ -419,14 +446,14 @@ struct capgen_engine {
   // the precomputed cross K/V.  q_done: q already projected (else bf16: the fused launch projects it
   // straight into the attention's LDS image, qkv_attn.hip cross mode).
   bool cross_fusable(int Lq) const {
-    return fused_qkv_on && act == DType::BF16 && L.dd == 512 && L.Hd * 64 == L.dd && Lq >= 1 && Lq <= 64;
+    return fused_qkv_on && act == DType::BF16 && wtile && L.dd == 512 && L.Hd * 64 == L.dd && Lq >= 1 && Lq <= 64;
   }
   void cross_attention(const AttnGeom& c, const void* D1, int64_t wq, int d, void* qc, void* attc, float* probs,
                        bool q_done, hipStream_t s) {
     if (!q_done) {
       QkvAttn qa;
       qa.g = c, qa.g.prio = prio(s), qa.cross = 1;
-      qa.X = reinterpret_cast<const bf16*>(D1), qa.ldx = d, qa.W = reinterpret_cast<const bf16*>(W(wq)), qa.ldw = d;
+      qa.X = reinterpret_cast<const bf16*>(D1), qa.ldx = d, qa.W = WT(wq);
       qa.d = d, qa.qkv = reinterpret_cast<bf16*>(qc), qa.ldqkv = d, qa.o = reinterpret_cast<bf16*>(attc);
       require(!probs && qkv_attn_ok(qa), "internal: cross-attention geometry the fused launch does not take");
       if (stamp_on) qa.g.stamp = stamp(s, "qkv_attn cross " + std::to_string(c.Lq) + "x" + std::to_string(c.Lk));
@@ -1123,6 +1150,7 @@ struct capgen_engine {
     const int64_t ns = shadow ? std::max<int64_t>(0, std::min(n, L.n_dense - off)) : 0;
     adam_update(params + off, grads + off, am + off, av + off, (size_t)n, cfg.beta1, cfg.beta2, cfg.eps, adam_scal,
                 ns > 0 ? shadow + off : nullptr, (size_t)ns, s, grid_cap);
+    if (ns > 0) retile(off, ns, s);
   }
   // Adam grid of the step's last buckets (embedding, encoder LN/biases), which sit between the
   // backward's end and the next forward: the common cap (0).  The whole chip for them measured
@@ -1173,6 +1201,7 @@ struct capgen_engine {
         NCCL_CHECK(ncclAllGather(params + o, params + off, (size_t)c, ncclFloat, comm, ec));
       }
       if (ns > 0) to_bf16(params + off, shadow + off, (size_t)ns, ec);
+      if (ns > 0) retile(off, ns, ec);
       return;
     }
     if (comm) {
@@ -1453,10 +1482,12 @@ struct capgen_engine {
     adam_prepare(step, cfg.lr, cfg.beta1, cfg.beta2, adam_scal, s);
     adam_update(params, grads, am, av, (size_t)L.total, cfg.beta1, cfg.beta2, cfg.eps, adam_scal, shadow,
                 shadow ? (size_t)L.n_dense : 0, s);
+    if (shadow) retile(0, L.n_dense, s);
   }
 
   void refresh_shadow(hipStream_t s) {
     if (shadow) to_bf16(params, shadow, (size_t)L.n_dense, s);
+    if (shadow) retile(0, L.n_dense, s);
   }
 
   // ------------------------------------------------------------------------------------
@@ -1928,7 +1959,7 @@ struct capgen_engine {
     if (es) (void)hipStreamSynchronize(es);
     drop_graph();
     if (comm) ncclCommDestroy(comm);
-    for (void* p : {(void*)params, (void*)grads, (void*)am, (void*)av, (void*)shadow, (void*)pe, (void*)step,
+    for (void* p : {(void*)params, (void*)grads, (void*)am, (void*)av, (void*)shadow, (void*)wtile, (void*)pe, (void*)step,
                     (void*)adam_scal, (void*)seed, (void*)scalars, (void*)gstripe, ws, gws, (void*)stamp_ring})
       if (p) (void)hipFree(p);
     if (count_host) (void)hipHostFree(count_host);
@@ -2051,6 +2082,7 @@ int capgen_create(const capgen_config* cfg, int device, capgen_t** out) {
     if (h->act == DType::BF16) {
       CAPGEN_HIP(hipMalloc(&h->shadow, (size_t)h->L.n_dense * 2));
       CAPGEN_HIP(hipMemset(h->shadow, 0, (size_t)h->L.n_dense * 2));
+      h->build_tiles();
     }
     std::vector<float> pe;
     pe_table(h->L, pe);
@@ -2346,6 +2378,21 @@ int capgen_debug_attention(int dtype, int B, int H, int Lq, int Lk, int dk, cons
   });
 }
 
+// the test hooks' weights in the fronts' tiled layout (a per-process scratch, grown as needed)
+static const bf16* debug_tiles(const bf16* W, int rows, hipStream_t s) {
+  static bf16* buf = nullptr;
+  static size_t cap = 0;
+  const size_t need = (size_t)rows * 512 * 2;
+  if (need > cap) {
+    CAPGEN_HIP(hipDeviceSynchronize());  // (the previous scratch may still be read)
+    if (buf) CAPGEN_HIP(hipFree(buf));
+    CAPGEN_HIP(hipMalloc(&buf, need));
+    cap = need;
+  }
+  qkv_tile_weights(W, rows, 512, buf, s);
+  return buf;
+}
+
 int capgen_debug_qkv_attention(int B, int L, int H, const void* X, const void* W, void* qkv, void* o,
                                const unsigned char* key_valid, const int32_t* key_ids, int pad_idx, int causal,
                                void* stream) {
@@ -2361,7 +2408,7 @@ int capgen_debug_qkv_attention(int B, int L, int H, const void* X, const void* W
     g.o_ld = d, g.o_bs = (int64_t)L * d;
     g.key_valid = key_valid, g.kv_bs = L, g.key_ids = key_ids, g.kid_bs = L, g.pad_idx = pad_idx, g.causal = causal;
     g.temperature = 8.f;  // sqrt(64)
-    qa.X = (const bf16*)X, qa.ldx = d, qa.W = (const bf16*)W, qa.ldw = d, qa.d = d;
+    qa.X = (const bf16*)X, qa.ldx = d, qa.W = debug_tiles((const bf16*)W, 3 * d, (hipStream_t)stream), qa.d = d;
     qa.qkv = (bf16*)qkv, qa.ldqkv = 3 * d, qa.o = (bf16*)o;
     qkv_attn_fwd(qa, (hipStream_t)stream);
   });
@@ -2382,7 +2429,7 @@ int capgen_debug_cross_attention(int B, int Lq, int Lk, int H, const void* X, co
     g.key_valid = key_valid, g.kv_bs = Lk;
     g.temperature = 8.f;
     qa.cross = 1;
-    qa.X = (const bf16*)X, qa.ldx = d, qa.W = (const bf16*)Wq, qa.ldw = d, qa.d = d;
+    qa.X = (const bf16*)X, qa.ldx = d, qa.W = debug_tiles((const bf16*)Wq, d, (hipStream_t)stream), qa.d = d;
     qa.qkv = (bf16*)q, qa.ldqkv = d, qa.o = (bf16*)o;
     qkv_attn_fwd(qa, (hipStream_t)stream);
   });

@@ -11,8 +11,7 @@ struct QkvAttn {
   AttnGeom g;
   const bf16* X = nullptr;  // row r of image b at X + (b * L + r) * ldx (cross: L = g.Lq)
   int64_t ldx = 0;
-  const bf16* W = nullptr;  // Wqkv [3d][ldw] (nn.Linear layout)
-  int64_t ldw = 0;
+  const bf16* W = nullptr;  // Wqkv (cross: Wq) in the tiled layout of qkv_tile_weights
   int d = 0;
   bf16* qkv = nullptr;  // [B * L][ldqkv]: q | k | v (null: not stored)
   int64_t ldqkv = 0;
@@ -22,6 +21,12 @@ struct QkvAttn {
   int cross = 0;
 };
 bool qkv_attn_ok(const QkvAttn& a);
+// The fronts read their projection weights TILED: the 64 lanes' 16-B MFMA fragments of 16-row block j
+// and 32-deep k-step ks (lane: row 16 j + (lane & 15), k = 32 ks + 8 (lane >> 4) .. + 7) are 1 KB
+// contiguous at dst + (16 j + ks) * 512 elements (K = 512).  A fragment load is then one coalesced
+// 1-KB piece (8 whole cache lines) instead of 16 rows x 64 B (measured: 19.3 -> 13.5 us per encoder
+// front launch, tools/front_microbench.py).  src: R rows (R % 16 == 0) of [R][ld], nn.Linear layout.
+void qkv_tile_weights(const bf16* src, int R, int64_t ld, bf16* dst, hipStream_t s);
 void qkv_attn_fwd(const QkvAttn& a, hipStream_t s);
 
 }  // namespace capgen

@@ -13,7 +13,10 @@
 //   * wave w computes 48 of the head's 192 projection columns (q | k | v, 64 each) for all rows:
 //     its B fragments (the weight rows) are private to it, so they come straight from global
 //     memory into registers, four 32-deep k-steps per batch, double buffered (the weights are
-//     re-read by every image: L2 / Infinity-Cache hits);
+//     re-read by every image: L2 / Infinity-Cache hits).  The weights are read in a TILED copy
+//     (qkv_tile_weights, kept current by the engine beside the bf16 shadow): each fragment load is
+//     one coalesced 1-KB piece -- from the row-major matrix a load touched 16 rows x 64 B and the
+//     launch was bound by those requests (19.3 vs 13.5 us per encoder launch, same work);
 //   * v_mfma_f32_16x16x32_bf16 with swapped operands (lane = one row, 4 consecutive columns), the
 //     same k order for A and B (standard order: lane group g holds k = 8g .. 8g+7);
 //   * the f32 results are rounded to bf16 once -- exactly the values a bf16 GEMM store would leave
@@ -65,17 +68,18 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
   // key flags; then the LDS writes: X (rows >= L zero), zeroed attention images.
   // Projection: wave w -> columns 48w .. 48w+47 of [q_h | k_h | v_h]. ----
   const int fr = lane & 15, fg = lane >> 4;
+  // (tiled weights: fragment f of this wave = 16-row block j of W, one 1-KB piece per k-step)
   const bf16* wrow[NF];
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
-    const int c = 16 * NF * w + 16 * f + fr, which = c >> 6, within = c & 63;
-    wrow[f] = a.W + (int64_t)(which * QD + h * DK + within) * a.ldw + 8 * fg;
+    const int c = 16 * NF * w + 16 * f, which = c >> 6, within = c & 63;
+    wrow[f] = a.W + ((int64_t)((which * QD + h * DK + within) >> 4) * QKS * 64 + lane) * 8;
   }
   bf16x8 bq[2][QKB][NF];
 #pragma unroll
   for (int kk = 0; kk < QKB; ++kk)
 #pragma unroll
-    for (int f = 0; f < NF; ++f) bq[0][kk][f] = *reinterpret_cast<const bf16x8*>(wrow[f] + 32 * kk);
+    for (int f = 0; f < NF; ++f) bq[0][kk][f] = *reinterpret_cast<const bf16x8*>(wrow[f] + 512 * kk);
   {
     constexpr int CH = LT * 16 * QD / 8;  // 16-B chunks of the staged rows
     constexpr int PER = CH / 256;
@@ -145,7 +149,7 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
       for (int kk = 0; kk < QKB; ++kk)
 #pragma unroll
         for (int f = 0; f < NF; ++f)
-          bq[cur ^ 1][kk][f] = *reinterpret_cast<const bf16x8*>(wrow[f] + 32 * ((grp + 1) * QKB + kk));
+          bq[cur ^ 1][kk][f] = *reinterpret_cast<const bf16x8*>(wrow[f] + 512 * ((grp + 1) * QKB + kk));
     }
     // the next batch's loads all issue before this batch's MFMAs (hipcc otherwise interleaves them
     // with partial waits and keeps only ~5 of the 12 in flight)
@@ -185,15 +189,35 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
   attn_fwd_staged(g, a.o, nullptr, b, h, sm);
 }
 
+__global__ void tile_weights_kernel(const bf16* __restrict__ src, int64_t n, int64_t ld, bf16* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // 16-B piece of dst
+  if (i >= n) return;
+  const int lane = (int)(i & 63), ks = (int)((i >> 6) % QKS);
+  const int64_t j = (i >> 6) / QKS;
+  const uint4 v = *reinterpret_cast<const uint4*>(src + (16 * j + (lane & 15)) * ld + 32 * ks + 8 * (lane >> 4));
+  reinterpret_cast<uint4*>(dst)[i] = v;
+}
+
 }  // namespace
+
+void qkv_tile_weights(const bf16* src, int R, int64_t ld, bf16* dst, hipStream_t s) {
+  require(R > 0 && R % 16 == 0 && ld % 8 == 0 && ld >= QD, "qkv_tile_weights: R % 16 == 0, ld >= 512");
+  if (hz::active()) {
+    using namespace hz;
+    hz::op(s, "qkv_tile_weights", {blk(src, R, QD * 2, ld * 2, RD), wr(dst, (int64_t)R * QD * 2)});
+  }
+  const int64_t n = (int64_t)R * QD / 8;
+  tile_weights_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(src, n, ld, dst);
+  CAPGEN_HIP(hipGetLastError());
+}
 
 bool qkv_attn_ok(const QkvAttn& a) {
   const AttnGeom& g = a.g;
   const bool shape = a.cross ? (g.Lk >= 1 && g.Lk <= 64 && g.k_ld % 8 == 0 && g.v_ld % 8 == 0 && g.k_bs % 8 == 0 &&
                                 g.v_bs % 8 == 0)
                              : (g.Lq == g.Lk && g.kv_bmod == 0);
-  return shape && g.dk == DK && g.H * DK == QD && a.d == QD && g.Lq >= 1 && g.Lq <= 64 && !g.kv_row &&
-         a.ldx % 8 == 0 && a.ldw % 8 == 0 && a.ldqkv % 8 == 0 && g.o_ld % 8 == 0 && g.o_bs % 8 == 0;
+  return shape && g.dk == DK && g.H * DK == QD && a.d == QD && g.Lq >= 1 && g.Lq <= 64 && !g.kv_row && a.W &&
+         a.ldx % 8 == 0 && a.ldqkv % 8 == 0 && g.o_ld % 8 == 0 && g.o_bs % 8 == 0;
 }
 
 void qkv_attn_fwd(const QkvAttn& a, hipStream_t s) {
@@ -204,7 +228,7 @@ void qkv_attn_fwd(const QkvAttn& a, hipStream_t s) {
     const int L = g.Lq;
     const int np = a.cross ? 1 : 3, Bk = g.kv_bmod > 0 ? std::min(g.B, g.kv_bmod) : g.B;
     const Rgn r[] = {rows_blk(a.X, g.B, L, (int64_t)L * a.ldx, a.ldx, a.d, 2, RD),
-                     rd(a.W, (int64_t)np * a.d * a.ldw * 2),
+                     rd(a.W, (int64_t)np * QD * QD * 2),
                      blk(g.key_valid, Bk, g.Lk, g.kv_bs, RD), blk(g.key_ids, g.B, (int64_t)g.Lk * 4, g.kid_bs * 4, RD),
                      rows_blk(a.cross ? g.k : nullptr, Bk, g.Lk, g.k_bs, g.k_ld, a.d, 2, RD),
                      rows_blk(a.cross ? g.v : nullptr, Bk, g.Lk, g.v_bs, g.v_ld, a.d, 2, RD),
