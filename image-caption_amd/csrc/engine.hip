@@ -93,7 +93,6 @@ struct Acts {
   float2* ce_stats;  // fused classifier + CE (bf16): {max, sum exp} per row and 16-column slab
   float* ce_tl;      // its target logits
   float *loss_row, *grad_scale, *loss, *loss_ce;
-  int* ce_ticket;    // ce_finish's last-workgroup ticket (zeroed at allocation, re-armed by the kernel)
   void* gEnc;     // encoder-chain residual gradient while decoder block 0 finishes on es2 (overlap_dec0)
   // SCST (rl.hip): per-row sample / lse / logp[sample] / entropy, per-image entropy, scalars
   int32_t* rl_sample;
@@ -586,7 +585,6 @@ struct capgen_engine {
     p.take(a.grad_scale, 4);
     p.take(a.loss, 4);
     p.take(a.loss_ce, 4);
-    p.take(a.ce_ticket, 1);
     T_(a.gEnc, Me * d);
     p.take(a.rl_sample, Md);
     p.take(a.rl_lse, Md);
@@ -687,7 +685,6 @@ struct capgen_engine {
     q.base = (char*)ws;
     plan_acts(q, nB, nN, nT);
     a.B = nB, a.N = nN, a.T = nT;
-    CAPGEN_HIP(hipMemsetAsync(a.ce_ticket, 0, sizeof(int), es));  // (ordered before any step on es)
   }
 
   void drop_graph() {
@@ -965,7 +962,6 @@ struct capgen_engine {
     if (L.has_mf)
       move_first_fwd(a.D[L.Ld], a.X[L.Le], Md, Lq, 0, N, a.mfU, a.mfH, a.tmp, a.mfOut, a.mfV, a.mfM, a.mfR, drop_on, s);
     // ---- classifier + CE (model.py:93-96) ----
-    float* lo = loss_out ? loss_out : a.loss;
     if (fused_ce()) {
       // the logits are never written: the GEMM epilogue leaves exp(v - slab max) + slab stats,
       // ce_finish turns them into the loss rows and softmax - onehot (model.py:93-96)
@@ -975,16 +971,13 @@ struct capgen_engine {
       ga.ce_stats = a.ce_stats, ga.ce_ld = (L.V + 15) / 16, ga.ce_tgt = a.tgt, ga.ce_tlogit = a.ce_tl;
       if (stamp_on) ga.stamp = stamp(s, "gemm classifier+CE " + dims(Md, L.V, dd));
       gemm(ga, act, act, false, false, s);
-      // (single process: ce_finish's last workgroup also finalises the loss and the gradient scale)
-      CeFinal fin;
-      if (!comm) fin.count = a.count, fin.focal = cfg.focal_loss, fin.loss_out = lo, fin.grad_scale = a.grad_scale;
-      if (!comm) fin.ticket = a.ce_ticket;
       ce_finish(a.ce_stats, (L.V + 15) / 16, a.ce_tl, a.tgt, Md, L.V, cfg.pad_idx, a.loss_row,
-                reinterpret_cast<bf16*>(a.dlogits), s, fin);
+                reinterpret_cast<bf16*>(a.dlogits), s);
     } else {
       linear(dec_out(), dd, L.Wc, dd, a.logits, L.V, DType::F32, Md, L.V, dd, P(L.bc), 0, s);
       cross_entropy_rows(a.logits, a.tgt, Md, L.V, cfg.pad_idx, a.loss_row, a.dlogits, act, s);
     }
+    float* lo = loss_out ? loss_out : a.loss;
     if (comm) {
       // data parallel: the mean CE over the GLOBAL batch (model.py:76) is the sum of the ranks'
       // partial sums / global count -- one 4-byte all-reduce, then the (Focal) loss and the
@@ -993,7 +986,7 @@ struct capgen_engine {
       nccl_op(s, "allreduce(ce)", a.loss_ce, 4);
       NCCL_CHECK(ncclAllReduce(a.loss_ce, a.loss_ce, 1, ncclFloat, ncclSum, comm, s));
       loss_finalize(nullptr, 0, a.count, cfg.focal_loss, lo, a.grad_scale, s, a.loss_ce);
-    } else if (!fused_ce()) {
+    } else {
       loss_finalize(a.loss_row, Md, a.count, cfg.focal_loss, lo, a.grad_scale, s);
     }
     stamp_fwd_end = stamp_next;

@@ -76,20 +76,10 @@ void stripe_reduce(float* S, int stripes, int64_t stride, int64_t n, float* dst,
 // per-row cross entropy: loss_row[m] = lse - logit[tgt], dlogits = softmax - onehot (unscaled, 0 for pad)
 void cross_entropy_rows(const float* logits, const int32_t* tgt, int M, int V, int pad, float* loss_row,
                         void* dlogits, DType t, hipStream_t s);
-// the loss finalisation run by ce_finish's last workgroup (loss_finalize's single-process form):
-// loss_out = CE mean over *count (FocalLoss when focal), grad_scale = its derivative / *count.
-// ticket: a device int, zero before the first use (re-armed by the kernel); null = not merged.
-struct CeFinal {
-  const float* count = nullptr;
-  int focal = 0;
-  float* loss_out = nullptr;
-  float* grad_scale = nullptr;
-  int* ticket = nullptr;
-};
 // fused classifier + CE, second half: dl holds exp(v - slab max) from the classifier GEMM's CE
 // epilogue (GemmArgs::ce_stats); writes loss_row and rewrites dl as softmax - onehot (0 for pad)
 void ce_finish(const float2* stats, int64_t ld, const float* tlogit, const int32_t* tgt, int M, int V, int pad,
-               float* loss_row, bf16* dl, hipStream_t s, const CeFinal& fin = CeFinal{});
+               float* loss_row, bf16* dl, hipStream_t s);
 // loss = sum(loss_row)/count (or FocalLoss of it); grad_scale = dloss/d(logit sums).
 // ce_in: the mean CE is given (all-reduced partials); partial: write sum(loss_row)/count only.
 void loss_finalize(const float* loss_row, int M, const float* count, int focal, float* loss_out,

@@ -653,47 +653,12 @@ void cross_entropy_rows(const float* logits, const int32_t* tgt, int M, int V, i
 // workgroup per row: lse = M + log sum_c s_c exp(mx_c - M), loss_row = lse - v[tgt], and the
 // row is rewritten in place as softmax - onehot = e * exp(mx_c - lse) - onehot.  Every load of the
 // row (stats + the thread's slabs) is issued up front: one memory round trip.
-// CE mean over the (global) non-pad count and the FocalLoss transform (model.py:73-76,
-// loss.py:20-28, gamma = 2, applied to the already-averaged CE).  ce_in != null: the mean CE is
-// given (the data-parallel path all-reduces the per-rank partial sums first); partial: only
-// the per-rank partial mean sum(rows) / count is written to loss_out.  256 threads; the row sum
-// runs in one fixed order (deterministic).
-__device__ __forceinline__ void loss_finalize_body(const float* loss_row, int M, const float* count, int focal,
-                                                   const float* ce_in, int partial, float* loss_out,
-                                                   float* grad_scale, float* sh) {
-  float acc = 0.f;
-  if (!ce_in)
-    for (int c = threadIdx.x; c < M; c += 256) acc += loss_row[c];
-  acc = block_sum(acc, sh);
-  if (threadIdx.x == 0) {
-    const float n = *count;
-    const float ce = ce_in ? *ce_in : acc / n;
-    if (partial) {
-      *loss_out = ce;
-    } else if (focal) {
-      const float pt = expf(-ce);
-      const float om = 1.f - pt;
-      *loss_out = om * om * ce;
-      *grad_scale = (2.f * om * pt * ce + om * om) / n;
-    } else {
-      *loss_out = ce;
-      *grad_scale = 1.f / n;
-    }
-  }
-}
-
-// fin.ticket != null: the loss finalisation runs in the same launch -- every workgroup takes a
-// ticket after its row's loss is stored (agent-scope acq_rel atomic: the store is released, the
-// last arriver acquires every other row's), and the workgroup drawing the last ticket re-arms it
-// and runs loss_finalize_body over all rows (one kernel boundary fewer on the step's critical path)
 template <int SPT>
 __global__ void __launch_bounds__(256) ce_finish_kernel(const float2* __restrict__ stats, int64_t ld,
                                                         const float* __restrict__ tlogit,
                                                         const int32_t* __restrict__ tgt, int V, int pad,
-                                                        float* __restrict__ loss_row, bf16* __restrict__ dl,
-                                                        CeFinal fin) {
+                                                        float* __restrict__ loss_row, bf16* __restrict__ dl) {
   __shared__ float sh[4];
-  __shared__ int last;
   typedef __attribute__((ext_vector_type(4))) __bf16 b4;
   const int m = blockIdx.x, nsl = (V + 15) / 16;
   bf16* row = dl + (int64_t)m * V;
@@ -713,74 +678,81 @@ __global__ void __launch_bounds__(256) ce_finish_kernel(const float2* __restrict
 #pragma unroll
   for (int u = 0; u < SPT; ++u)
     if (threadIdx.x + 256 * u >= nsl) st[u] = float2{-INFINITY, 0.f};
-  float lrow = 0.f;
   if (y == pad) {  // (uniform per workgroup)
     for (int c = threadIdx.x * 4; c < V; c += 256 * 4) *reinterpret_cast<b4*>(row + c) = b4{0, 0, 0, 0};
-  } else {
-    float mx = -INFINITY;
-#pragma unroll
-    for (int u = 0; u < SPT; ++u) mx = fmaxf(mx, st[u].x);
-    mx = block_max(mx, sh);
-    float se = 0.f;
-#pragma unroll
-    for (int u = 0; u < SPT; ++u) se += st[u].y == 0.f ? 0.f : st[u].y * expf(st[u].x - mx);
-    se = block_sum(se, sh);
-    const float lse = mx + logf(se);
-#pragma unroll
-    for (int u = 0; u < SPT; ++u) {
-      const int c = threadIdx.x + 256 * u;
-      if (c >= nsl) continue;
-      const float f = expf(st[u].x - lse);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int col = c * 16 + q * 4;
-        if (col >= V) continue;
-        float o[4] = {(float)e[u][q][0] * f, (float)e[u][q][1] * f, (float)e[u][q][2] * f, (float)e[u][q][3] * f};
-        if (y >= col && y < col + 4) o[y - col] -= 1.f;
-        *reinterpret_cast<b4*>(row + col) = b4{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
-      }
-    }
-    lrow = lse - tl;
-  }
-  if (!fin.ticket) {
-    if (threadIdx.x == 0) loss_row[m] = lrow;
+    if (threadIdx.x == 0) loss_row[m] = 0.f;
     return;
   }
-  if (threadIdx.x == 0) {
-    loss_row[m] = lrow;
-    const int old = __hip_atomic_fetch_add(fin.ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    last = old == (int)gridDim.x - 1;
-    if (last) (void)__hip_atomic_exchange(fin.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  float mx = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < SPT; ++u) mx = fmaxf(mx, st[u].x);
+  mx = block_max(mx, sh);
+  float se = 0.f;
+#pragma unroll
+  for (int u = 0; u < SPT; ++u) se += st[u].y == 0.f ? 0.f : st[u].y * expf(st[u].x - mx);
+  se = block_sum(se, sh);
+  const float lse = mx + logf(se);
+#pragma unroll
+  for (int u = 0; u < SPT; ++u) {
+    const int c = threadIdx.x + 256 * u;
+    if (c >= nsl) continue;
+    const float f = expf(st[u].x - lse);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int col = c * 16 + q * 4;
+      if (col >= V) continue;
+      float o[4] = {(float)e[u][q][0] * f, (float)e[u][q][1] * f, (float)e[u][q][2] * f, (float)e[u][q][3] * f};
+      if (y >= col && y < col + 4) o[y - col] -= 1.f;
+      *reinterpret_cast<b4*>(row + col) = b4{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+    }
   }
-  __syncthreads();
-  if (!last) return;
-  loss_finalize_body(loss_row, gridDim.x, fin.count, fin.focal, nullptr, 0, fin.loss_out, fin.grad_scale, sh);
+  if (threadIdx.x == 0) loss_row[m] = lse - tl;
 }
 void ce_finish(const float2* stats, int64_t ld, const float* tlogit, const int32_t* tgt, int M, int V, int pad,
-               float* loss_row, bf16* dl, hipStream_t s, const CeFinal& fin) {
+               float* loss_row, bf16* dl, hipStream_t s) {
   if (M <= 0) return;
   require(V % 4 == 0 && ld >= (V + 15) / 16, "ce_finish: V must be a multiple of 4");
   if (hz::active()) {
     using namespace hz;
     op(s, "ce_finish", {blk(stats, M, (int64_t)((V + 15) / 16) * 8, ld * 8, RD), rd(tlogit, (int64_t)M * 4),
-                        rd(tgt, (int64_t)M * 4), wr(loss_row, (int64_t)M * 4), wr(dl, (int64_t)M * V * 2),
-                        rd(fin.ticket ? fin.count : nullptr, 4), blk(fin.ticket, 1, 4, 4, ACC),
-                        wr(fin.ticket ? fin.loss_out : nullptr, 4), wr(fin.ticket ? fin.grad_scale : nullptr, 4)});
+                        rd(tgt, (int64_t)M * 4), wr(loss_row, (int64_t)M * 4), wr(dl, (int64_t)M * V * 2)});
   }
   const int spt = ((V + 15) / 16 + 255) / 256;
-  if (spt <= 1) ce_finish_kernel<1><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl, fin);
-  else if (spt <= 2) ce_finish_kernel<2><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl, fin);
-  else if (spt <= 3) ce_finish_kernel<3><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl, fin);
-  else if (spt <= 4) ce_finish_kernel<4><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl, fin);
-  else if (spt <= 8) ce_finish_kernel<8><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl, fin);
+  if (spt <= 1) ce_finish_kernel<1><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl);
+  else if (spt <= 2) ce_finish_kernel<2><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl);
+  else if (spt <= 3) ce_finish_kernel<3><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl);
+  else if (spt <= 4) ce_finish_kernel<4><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl);
+  else if (spt <= 8) ce_finish_kernel<8><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl);
   else throw Error("ce_finish: V > 32768");
   CAPGEN_HIP(hipGetLastError());
 }
 
+// CE mean over the (global) non-pad count and the FocalLoss transform (model.py:73-76,
+// loss.py:20-28, gamma = 2, applied to the already-averaged CE).  ce_in != null: the mean CE is
+// given (the data-parallel path all-reduces the per-rank partial sums first); partial: only
+// the per-rank partial mean sum(rows) / count is written to loss_out.
 __global__ void loss_finalize_kernel(const float* __restrict__ loss_row, int M, const float* count, int focal,
                                      const float* ce_in, int partial, float* loss_out, float* grad_scale) {
   __shared__ float sh[4];
-  loss_finalize_body(loss_row, M, count, focal, ce_in, partial, loss_out, grad_scale, sh);
+  float acc = 0.f;
+  if (!ce_in)
+    for (int c = threadIdx.x; c < M; c += 256) acc += loss_row[c];
+  acc = block_sum(acc, sh);
+  if (threadIdx.x == 0) {
+    const float n = *count;
+    const float ce = ce_in ? *ce_in : acc / n;
+    if (partial) {
+      *loss_out = ce;
+    } else if (focal) {
+      const float pt = expf(-ce);
+      const float om = 1.f - pt;
+      *loss_out = om * om * ce;
+      *grad_scale = (2.f * om * pt * ce + om * om) / n;
+    } else {
+      *loss_out = ce;
+      *grad_scale = 1.f / n;
+    }
+  }
 }
 void loss_finalize(const float* loss_row, int M, const float* count, int focal, float* loss_out, float* grad_scale,
                    hipStream_t s, const float* ce_in, int partial) {
