@@ -1141,9 +1141,21 @@ struct capgen_engine {
   // Adam over arena ranges; ranges are 64-element aligned so the bf16 shadow slices line up
   void adam_range(int64_t off, int64_t n, hipStream_t s, int grid_cap = 0) {
     const int64_t ns = shadow ? std::max<int64_t>(0, std::min(n, L.n_dense - off)) : 0;
+    // the fronts' tiled weights in this range: written by the Adam kernel itself (else re-tiled after)
+    AdamTiles at;
+    bool fused_tiles = true;
+    for (auto& kv : tiled)
+      if (ns > 0 && kv.first >= off && kv.first < off + ns) {
+        if (at.n == AdamTiles::kMax) {
+          fused_tiles = false;
+          break;
+        }
+        at.off[at.n] = kv.first - off, at.len[at.n] = (int64_t)kv.second.second * 512;
+        at.dst[at.n++] = wtile + kv.second.first;
+      }
     adam_update(params + off, grads + off, am + off, av + off, (size_t)n, cfg.beta1, cfg.beta2, cfg.eps, adam_scal,
-                ns > 0 ? shadow + off : nullptr, (size_t)ns, s, grid_cap);
-    if (ns > 0) retile(off, ns, s);
+                ns > 0 ? shadow + off : nullptr, (size_t)ns, s, grid_cap, fused_tiles ? at : AdamTiles{});
+    if (ns > 0 && !fused_tiles) retile(off, ns, s);
   }
   // Adam grid of the step's last buckets (embedding, encoder LN/biases), which sit between the
   // backward's end and the next forward: the common cap (0).  The whole chip for them measured

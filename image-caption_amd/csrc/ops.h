@@ -86,8 +86,18 @@ void loss_finalize(const float* loss_row, int M, const float* count, int focal, 
                    float* grad_scale, hipStream_t s, const float* ce_in = nullptr, int partial = 0);
 // Adam (torch.optim.Adam semantics).  step_buf: int64 step counter (incremented here).
 void adam_prepare(int64_t* step, float lr, float b1, float b2, float* scal, hipStream_t s);
+// Ranges of the shadow (relative to p, element offsets) that adam_update also writes in the fused
+// attention fronts' tiled layout (qkv_tile_weights) -- whole 16-row blocks of 512-wide rows
+struct AdamTiles {
+  static constexpr int kMax = 4;
+  int n = 0;
+  int64_t off[kMax] = {};
+  int64_t len[kMax] = {};
+  bf16* dst[kMax] = {};
+};
 void adam_update(float* p, const float* g, float* m, float* v, size_t n, float b1, float b2, float eps,
-                 const float* scal, bf16* shadow, size_t n_shadow, hipStream_t s, int grid_cap = 0);
+                 const float* scal, bf16* shadow, size_t n_shadow, hipStream_t s, int grid_cap = 0,
+                 const AdamTiles& tiles = AdamTiles{});
 void to_bf16(const float* src, bf16* dst, size_t n, hipStream_t s);
 // greedy: out token = argmax(softmax(logits[b])) (first index on ties)   (model.py:126-128)
 void argmax_softmax(const float* logits, int B, int V, int64_t* ids_out, int64_t ids_ld, int col,

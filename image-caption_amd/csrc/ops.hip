@@ -781,7 +781,7 @@ void adam_prepare(int64_t* step, float lr, float b1, float b2, float* scal, hipS
 __global__ void __launch_bounds__(256) adam_kernel(float4* __restrict__ p, const float4* __restrict__ g,
                                                    float4* __restrict__ m, float4* __restrict__ v, size_t n4,
                                                    float b1, float b2, float eps, const float* __restrict__ scal,
-                                                   bf16* __restrict__ shadow, size_t n_shadow) {
+                                                   bf16* __restrict__ shadow, size_t n_shadow, AdamTiles tiles) {
   const float neg_step = scal[0], bc2s = scal[1];
   const float b1c = 1.f - b1, b2c = 1.f - b2;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
@@ -797,16 +797,38 @@ __global__ void __launch_bounds__(256) adam_kernel(float4* __restrict__ p, const
       typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
       bf16x4 o = {(bf16)pp.x, (bf16)pp.y, (bf16)pp.z, (bf16)pp.w};
       *reinterpret_cast<bf16x4*>(shadow + 4 * i) = o;
+      // the fused attention fronts' tiled copy (qkv_tile_weights layout): 4 consecutive k of one
+      // row land in one 8-B piece of the row's 16-B fragment slot
+#pragma unroll
+      for (int t = 0; t < AdamTiles::kMax; ++t) {
+        const int64_t rel = (int64_t)(4 * i) - tiles.off[t];
+        if (t < tiles.n && rel >= 0 && rel < tiles.len[t]) {
+          const int64_t row = rel >> 9;
+          const int k = (int)(rel & 511);
+          const int64_t piece = (((row >> 4) * 16 + (k >> 5)) * 64 + (row & 15) + 16 * ((k >> 3) & 3)) * 8 + (k & 7);
+          *reinterpret_cast<bf16x4*>(tiles.dst[t] + piece) = o;
+        }
+      }
     }
   }
 }
 void adam_update(float* p, const float* g, float* m, float* v, size_t n, float b1, float b2, float eps,
-                 const float* scal, bf16* shadow, size_t n_shadow, hipStream_t s, int grid_cap) {
+                 const float* scal, bf16* shadow, size_t n_shadow, hipStream_t s, int grid_cap,
+                 const AdamTiles& tiles) {
+  require(tiles.n >= 0 && tiles.n <= AdamTiles::kMax, "adam: at most kMax tiled ranges");
+  for (int t = 0; t < tiles.n; ++t)
+    require(shadow && tiles.off[t] % 512 == 0 && tiles.len[t] % (16 * 512) == 0 && tiles.off[t] >= 0 &&
+                tiles.off[t] + tiles.len[t] <= (int64_t)n_shadow && tiles.dst[t],
+            "adam: a tiled range must be whole 16-row blocks of 512-wide rows inside the shadow range");
   require(n % 4 == 0 && n_shadow % 4 == 0, "adam: arena size must be a multiple of 4");
   if (skip_mask() & 32) return;
   if (hz::active())
     hz::op(s, "adam", {hz::rd(g, (int64_t)n * 4), hz::rd(scal, 8), hz::wr(p, (int64_t)n * 4), hz::wr(m, (int64_t)n * 4),
-                       hz::wr(v, (int64_t)n * 4), hz::wr(shadow, (int64_t)n_shadow * 2)});
+                       hz::wr(v, (int64_t)n * 4), hz::wr(shadow, (int64_t)n_shadow * 2),
+                       hz::wr(tiles.n > 0 ? tiles.dst[0] : nullptr, tiles.n > 0 ? tiles.len[0] * 2 : 0),
+                       hz::wr(tiles.n > 1 ? tiles.dst[1] : nullptr, tiles.n > 1 ? tiles.len[1] * 2 : 0),
+                       hz::wr(tiles.n > 2 ? tiles.dst[2] : nullptr, tiles.n > 2 ? tiles.len[2] * 2 : 0),
+                       hz::wr(tiles.n > 3 ? tiles.dst[3] : nullptr, tiles.n > 3 ? tiles.len[3] * 2 : 0)});
   size_t n4 = n / 4;
   static const int cap = [] {  // Adam workgroups (grid-stride): one per CU leaves the other wave slots to the
     // critical stream (A/B over 4 runs each: 3.046 vs 3.070 ms/step with 8 per CU; CAPGEN_ADAM_GRID)
@@ -816,7 +838,7 @@ void adam_update(float* p, const float* g, float* m, float* v, size_t n, float b
   // grid_cap > 0: the caller's cap (an update on the step's critical path takes the whole chip)
   int grid = (int)std::min<size_t>((n4 + 255) / 256, (size_t)(grid_cap > 0 ? grid_cap : cap));
   adam_kernel<<<grid, 256, 0, s>>>((float4*)p, (const float4*)g, (float4*)m, (float4*)v, n4, b1, b2, eps, scal,
-                                   shadow, n_shadow);
+                                   shadow, n_shadow, tiles);
   CAPGEN_HIP(hipGetLastError());
 }
 
