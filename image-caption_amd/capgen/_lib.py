@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CAPGEN_LIB_PATH") or os.path.join(_HERE, "libcapgen.so")  # (diagnostic builds)
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 F32, BF16 = 0, 1
 
@@ -81,6 +81,8 @@ _SIGS = {
     "capgen_rl_finish": (C.c_int, [_P, _P, C.c_float, _P, C.c_int, _P]),
     "capgen_debug_attention": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P,
                                          C.c_int, C.c_float, _P, _P, _P, _P, _P, _P, _P]),
+    "capgen_debug_attention_bwd_wo": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int, _P, _P,
+                                                _P, _P, _P, _P]),
     "capgen_debug_qkv_attention": (C.c_int, [C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, C.c_int, C.c_int, _P]),
     "capgen_debug_cross_attention": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P]),
     "capgen_dp_unique_id": (C.c_int, [C.c_char_p]),

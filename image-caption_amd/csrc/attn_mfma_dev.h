@@ -198,6 +198,98 @@ __device__ __forceinline__ void attn_fwd_one(const AttnGeom& g, bf16* __restrict
   attn_fwd_staged(g, o, probs, b, h, sm);
 }
 
+// backward of one (batch b, head h) once K / dO / Q / V sit in their LDS images and the key flags in
+// kok (zero rows beyond Lq / Lk); Pdimg / dSimg are scratch images.  256 threads; the workgroup
+// barrier inside is reached by every wave.
+__device__ __forceinline__ void attn_bwd_staged(const AttnGeom& g, bf16* __restrict__ dq, bf16* __restrict__ dkp,
+                                                bf16* __restrict__ dvp, int b, int h, const char* Kimg,
+                                                const char* dOimg, const char* Qimg, const char* Vimg, char* Pdimg,
+                                                char* dSimg, const unsigned char* kok) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t qoff = (int64_t)b * g.q_bs + h * DK, koff = (int64_t)b * g.k_bs + h * DK,
+                voff = (int64_t)b * g.v_bs + h * DK;
+  // ---- phase 1: wave w = query rows 16w..16w+15 ----
+  const int q0 = 16 * w, q = q0 + (lane & 15);
+  const float inv_t = 1.f / g.temperature;
+  f32x4 ds[4], pd[4];
+  if (q0 < g.Lq) {
+    f32x4 s[4], p[4], dp[4];
+    scores(Qimg, q0, Kimg, lane, s);
+    softmax_rows(g, kok, q, lane, s, p);
+    scores(dOimg, q0, Vimg, lane, dp);  // d(p_dropped) = dO . V^T
+    const int64_t row_idx = (((int64_t)b * g.H + h) * g.Lq + q) * g.Lk;
+    const uint64_t seed = g.drop.seed_ptr ? *g.drop.seed_ptr : 0;
+    float rs = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = 16 * j + 4 * (lane >> 4) + r;
+        float d = dp[j][r], pp = p[j][r];
+        if (g.drop.seed_ptr) {
+          const bool keep = drop_keep(seed, g.drop.site, (uint32_t)(row_idx + key), g.drop.thresh);
+          d = keep ? d * g.drop.scale : 0.f;
+          pp = keep ? pp * g.drop.scale : 0.f;
+        }
+        dp[j][r] = d;
+        pd[j][r] = pp;
+        rs += p[j][r] * d;
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    const bool live = q < g.Lq;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        ds[j][r] = live ? p[j][r] * (dp[j][r] - rs) : 0.f;  // softmax backward
+        pd[j][r] = live ? pd[j][r] : 0.f;
+      }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ds[j] = pd[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    put4(Pdimg, q, 16 * j + 4 * (lane >> 4), pd[j]);
+    put4(dSimg, q, 16 * j + 4 * (lane >> 4), ds[j]);
+  }
+  __syncthreads();
+  if (q0 < g.Lq) {  // dQ^T[d][q] = K^T[d][key] . dS^T[key][q]
+    const bf16x8 f0 = pack8(ds[0], ds[1]), f1 = pack8(ds[2], ds[3]);
+    bf16* dqb = dq + qoff;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_t(Kimg, 16 * t, 0, lane), f0, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_t(Kimg, 16 * t, 1, lane), f1, acc, 0, 0, 0);
+      if (q < g.Lq) store4(dqb + (int64_t)q * g.q_ld + 16 * t + 4 * (lane >> 4), acc, inv_t);
+    }
+  }
+  // ---- phase 2: wave w = key rows 16w..16w+15; K dimension = query rows ----
+  const int k0 = 16 * w;
+  if (k0 >= g.Lk) return;
+  const int key = k0 + (lane & 15);
+  const int nks = (g.Lq + 31) / 32;
+  bf16* dvb = dvp + voff;
+  bf16* dkb = dkp + koff;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    f32x4 av = f32x4{0.f, 0.f, 0.f, 0.f}, ak = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < nks; ++ks) {
+      // dV^T[d][key] = dO^T[d][q] . Pd[q][key];  dK^T[d][key] = Q^T[d][q] . dS[q][key]
+      av = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_t(dOimg, 16 * t, ks, lane), frag_t(Pdimg, k0, ks, lane), av,
+                                                   0, 0, 0);
+      ak = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_t(Qimg, 16 * t, ks, lane), frag_t(dSimg, k0, ks, lane), ak,
+                                                   0, 0, 0);
+    }
+    if (key < g.Lk) {
+      store4(dvb + (int64_t)key * g.v_ld + 16 * t + 4 * (lane >> 4), av, 1.f);
+      store4(dkb + (int64_t)key * g.k_ld + 16 * t + 4 * (lane >> 4), ak, inv_t);
+    }
+  }
+}
+
 constexpr int kFwdSmem = 3 * IMG + 64;
 
 }  // namespace amf

@@ -182,28 +182,38 @@ struct capgen_engine {
   // the fused attention fronts' weights (every self-attention Wqkv, every cross Wq) in the tiled
   // layout of qkv_tile_weights, re-tiled from the shadow wherever the shadow is written
   bf16* wtile = nullptr;
-  std::map<int64_t, std::pair<int64_t, int>> tiled;  // arena offset -> (element offset in wtile, rows)
+  // arena offset -> (element offset in wtile, rows); rows < 0: an output projection Wo [512][512]
+  // kept as the tiled Wo^T (the fused attention backward's dO = dA . Wo[:, head], qkv_attn_bwd)
+  std::map<int64_t, std::pair<int64_t, int>> tiled;
   const bf16* WT(int64_t woff) const {
     auto it = tiled.find(woff);
-    return it == tiled.end() ? nullptr : wtile + it->second.first;
+    return it == tiled.end() || it->second.second < 0 ? nullptr : wtile + it->second.first;
+  }
+  const bf16* WTo(int64_t woff) const {
+    auto it = tiled.find(woff);
+    return it == tiled.end() || it->second.second > 0 ? nullptr : wtile + it->second.first;
   }
   void build_tiles() {  // (bf16 engines, at creation: model widths of 512 only)
     std::vector<std::pair<int64_t, int>> ws;
     if (L.d == 512) {
-      for (const auto& e : L.enc) ws.push_back({e.Wqkv, 3 * L.d});
-      if (L.has_img) ws.push_back({L.img.Wqkv, 3 * L.d});
+      for (const auto& e : L.enc) ws.push_back({e.Wqkv, 3 * L.d}), ws.push_back({e.Wo, -512});
+      if (L.has_img) ws.push_back({L.img.Wqkv, 3 * L.d}), ws.push_back({L.img.Wo, -512});
     }
     if (L.dd == 512)
-      for (const auto& e : L.dec) ws.push_back({e.Wqkv, 3 * L.dd}), ws.push_back({e.Wq_c, L.dd});
+      for (const auto& e : L.dec)
+        ws.push_back({e.Wqkv, 3 * L.dd}), ws.push_back({e.Wq_c, L.dd}), ws.push_back({e.Wo_s, -512}),
+            ws.push_back({e.Wo_c, -512});
     int64_t n = 0;
-    for (auto& w : ws) tiled[w.first] = {n, w.second}, n += (int64_t)w.second * 512;
+    for (auto& w : ws) tiled[w.first] = {n, w.second}, n += (int64_t)std::abs(w.second) * 512;
     if (n) CAPGEN_HIP(hipMalloc(&wtile, (size_t)n * 2));
   }
   // re-tile the fronts' weights inside the arena range [off, off + n) from the shadow
-  void retile(int64_t off, int64_t n, hipStream_t s) {
+  void retile(int64_t off, int64_t n, hipStream_t s, bool trans_only = false) {
     for (auto& kv : tiled)
-      if (kv.first >= off && kv.first < off + n)
-        qkv_tile_weights(shadow + kv.first, kv.second.second, 512, wtile + kv.second.first, s);
+      if (kv.first >= off && kv.first < off + n) {
+        if (kv.second.second < 0) qkv_tile_weights_t(shadow + kv.first, 512, wtile + kv.second.first, s);
+        else if (!trans_only) qkv_tile_weights(shadow + kv.first, kv.second.second, 512, wtile + kv.second.first, s);
+      }
   }
   float* pe = nullptr;  // [max_length-1, dd] f32 sinusoid table
   int64_t* step = nullptr;
@@ -1137,6 +1147,32 @@ struct capgen_engine {
     dw_side(lb.d_a, d, att, d, Wo, d, M, d, d, nullptr, s);
     linear_dx(lb.d_a, d, Wo, d, gATT, d, M, d, d, 0, nullptr, nullptr, s);
   }
+  // ... followed by the attention backward of g: in bf16 with the tiled Wo^T, the projection's input
+  // gradient (dO = dA . Wo, dA = lb.d_a) runs INSIDE the attention backward launch (qkv_attn_bwd):
+  // one launch and one dependent boundary fewer per attention block (CAPGEN_FUSED_ATTN_BWD=0: the
+  // dX GEMM into gATT and the attention backward launch)
+  bool fused_attn_bwd_on = [] {
+    const char* e = std::getenv("CAPGEN_FUSED_ATTN_BWD");
+    return !(e && e[0] == '0');
+  }();
+  void mha_bwd(int M, int d, const LnBwd& lb, const void* att, int64_t Wo, void* gATT, const AttnGeom& g,
+               const float* probs, void* dq, void* dk, void* dv, hipStream_t s) {
+    if (fused_attn_bwd_on && act == DType::BF16 && WTo(Wo) && attention_mfma_ok(g)) {
+      QkvBwd qb;
+      qb.g = g, qb.g.prio = prio(s);
+      qb.dA = reinterpret_cast<const bf16*>(lb.d_a), qb.ldda = d, qb.Wt = WTo(Wo);
+      qb.dq = reinterpret_cast<bf16*>(dq), qb.dk = reinterpret_cast<bf16*>(dk), qb.dv = reinterpret_cast<bf16*>(dv);
+      if (qkv_bwd_ok(qb)) {
+        lnb(lb, s);
+        dw_side(lb.d_a, d, att, d, Wo, d, M, d, d, nullptr, s);
+        if (stamp_on) qb.g.stamp = stamp(s, "attn_bwd_wo " + std::to_string(g.Lq) + "x" + std::to_string(g.Lk));
+        qkv_attn_bwd(qb, s);
+        return;
+      }
+    }
+    mha_out_bwd(M, d, lb, att, Wo, gATT, s);
+    attb(g, probs, gATT, dq, dk, dv, act, s);
+  }
 
   // Adam over arena ranges; ranges are 64-element aligned so the bf16 shadow slices line up
   void adam_range(int64_t off, int64_t n, hipStream_t s, int grid_cap = 0) {
@@ -1145,7 +1181,7 @@ struct capgen_engine {
     AdamTiles at;
     bool fused_tiles = true;
     for (auto& kv : tiled)
-      if (ns > 0 && kv.first >= off && kv.first < off + ns) {
+      if (ns > 0 && kv.second.second > 0 && kv.first >= off && kv.first < off + ns) {
         if (at.n == AdamTiles::kMax) {
           fused_tiles = false;
           break;
@@ -1155,7 +1191,7 @@ struct capgen_engine {
       }
     adam_update(params + off, grads + off, am + off, av + off, (size_t)n, cfg.beta1, cfg.beta2, cfg.eps, adam_scal,
                 ns > 0 ? shadow + off : nullptr, (size_t)ns, s, grid_cap, fused_tiles ? at : AdamTiles{});
-    if (ns > 0 && !fused_tiles) retile(off, ns, s);
+    if (ns > 0) retile(off, ns, s, /*trans_only=*/fused_tiles);  // (the transposed ones: always a launch)
   }
   // Adam grid of the step's last buckets (embedding, encoder LN/biases), which sit between the
   // backward's end and the next forward: the common cap (0).  The whole chip for them measured
@@ -1253,8 +1289,7 @@ struct capgen_engine {
     if (valid) g.key_valid = valid, g.kv_bs = N, g.causal = 1;
     g.temperature = std::sqrt((float)dke);
     g.drop = mk_drop(pa, site(0, layer, 0), on);
-    mha_out_bwd(Me, d, lmha, A.att, w.Wo, gb.gATT1, s);
-    attb(g, A.P, gb.gATT1, gb.gQKV, at(gb.gQKV, d), at(gb.gQKV, 2 * d), act, s);
+    mha_bwd(Me, d, lmha, A.att, w.Wo, gb.gATT1, g, A.P, gb.gQKV, at(gb.gQKV, d), at(gb.gQKV, 2 * d), s);
     dw_side(gb.gQKV, 3 * d, X, d, w.Wqkv, d, Me, 3 * d, d, nullptr, s);
     linear_dx(gb.gQKV, 3 * d, w.Wqkv, d, go, d, Me, 3 * d, d, 1, nullptr, nullptr, s);  // gO = grad wrt X
   }
@@ -1379,8 +1414,9 @@ struct capgen_engine {
       c.key_valid = a.valid, c.kv_bs = N;  // masks as in forward (the MFMA backward recomputes P)
       c.temperature = std::sqrt((float)dkd);
       c.drop = mk_drop(pa, site(1, l, 5), on);
-      mha_out_bwd(Md, dd, lcross, A.attc, w.Wo_c, gb.gATT2, s);  // gO = grad wrt D1 (residual part)
-      attb(c, A.Pc, gb.gATT2, gb.gQc, at(a.gKV, (int64_t)l * 2 * dd), at(a.gKV, (int64_t)l * 2 * dd + dd), act, s);
+      // (lcross.d_res = grad wrt D1, the residual part)
+      mha_bwd(Md, dd, lcross, A.attc, w.Wo_c, gb.gATT2, c, A.Pc, gb.gQc, at(a.gKV, (int64_t)l * 2 * dd),
+              at(a.gKV, (int64_t)l * 2 * dd + dd), s);
       // block 0: the rest of the block runs on es2 (ov), the encoder chain starts on s below
       const bool ov = l == 0 && overlap_dec0 && es2 != s;
       const hipStream_t hs = ov ? es2 : s;
@@ -1396,8 +1432,8 @@ struct capgen_engine {
       g.key_ids = a.ids, g.kid_bs = Lq, g.pad_idx = cfg.pad_idx, g.causal = 1;  // as in forward
       g.temperature = std::sqrt((float)dkd);
       g.drop = mk_drop(pa, site(1, l, 3), on);
-      mha_out_bwd(Md, dd, lself, A.atts, w.Wo_s, gb.gATT1, hs);  // gR = grad wrt D_l (residual part)
-      attb(g, A.Ps, gb.gATT1, gb.gQKV, at(gb.gQKV, dd), at(gb.gQKV, 2 * dd), act, hs);
+      // (lself.d_res = grad wrt D_l, the residual part)
+      mha_bwd(Md, dd, lself, A.atts, w.Wo_s, gb.gATT1, g, A.Ps, gb.gQKV, at(gb.gQKV, dd), at(gb.gQKV, 2 * dd), hs);
       dw_side(gb.gQKV, 3 * dd, a.D[l], dd, w.Wqkv, dd, Md, 3 * dd, dd, nullptr, hs);
       linear_dx(gb.gQKV, 3 * dd, w.Wqkv, dd, gR, dd, Md, 3 * dd, dd, 1, nullptr, nullptr, hs);
       if (l % bucket_blocks == 0)  // blocks l .. l + bucket_blocks - 1 (contiguous in the arena)
@@ -2437,6 +2473,32 @@ int capgen_debug_cross_attention(int B, int Lq, int Lk, int H, const void* X, co
     qa.X = (const bf16*)X, qa.ldx = d, qa.W = debug_tiles((const bf16*)Wq, d, (hipStream_t)stream), qa.d = d;
     qa.qkv = (bf16*)q, qa.ldqkv = d, qa.o = (bf16*)o;
     qkv_attn_fwd(qa, (hipStream_t)stream);
+  });
+}
+
+int capgen_debug_attention_bwd_wo(int B, int Lq, int Lk, int H, const void* q, const void* k, const void* v,
+                                  const unsigned char* key_valid, int causal, const void* dA, const void* Wo, void* dq,
+                                  void* dk, void* dv, void* stream) {
+  return guarded([&] {
+    require(B >= 1 && Lq >= 1 && Lk >= 1 && H * 64 == 512, "debug_attention_bwd_wo: bad shape (H * 64 = 512)");
+    const int d = H * 64;
+    const hipStream_t s = (hipStream_t)stream;
+    static bf16* wt = nullptr;  // (the test hook's tiled Wo^T scratch)
+    if (!wt) CAPGEN_HIP(hipMalloc(&wt, (size_t)512 * 512 * 2));
+    qkv_tile_weights_t((const bf16*)Wo, 512, wt, s);
+    QkvBwd qb;
+    AttnGeom& g = qb.g;
+    g.B = B, g.H = H, g.Lq = Lq, g.Lk = Lk, g.dk = 64;
+    g.q = q, g.q_ld = d, g.q_bs = (int64_t)Lq * d;
+    g.k = k, g.k_ld = d, g.k_bs = (int64_t)Lk * d;
+    g.v = v, g.v_ld = d, g.v_bs = (int64_t)Lk * d;
+    g.o_ld = d, g.o_bs = (int64_t)Lq * d;
+    if (key_valid) g.key_valid = key_valid, g.kv_bs = Lk;
+    g.causal = causal;
+    g.temperature = 8.f;
+    qb.dA = (const bf16*)dA, qb.ldda = d, qb.Wt = wt;
+    qb.dq = (bf16*)dq, qb.dk = (bf16*)dk, qb.dv = (bf16*)dv;
+    qkv_attn_bwd(qb, s);
   });
 }
 

@@ -29,4 +29,24 @@ bool qkv_attn_ok(const QkvAttn& a);
 void qkv_tile_weights(const bf16* src, int R, int64_t ld, bf16* dst, hipStream_t s);
 void qkv_attn_fwd(const QkvAttn& a, hipStream_t s);
 
+// The output side of an attention block's backward in ONE launch per (image, head): dO_h = dA_b .
+// Wo[:, 64h .. 64h + 63] -- the input gradient of the output projection (modules.py:77 o_linear;
+// dA = the gradient at the projection's output) read through the tiled Wo^T -- straight into the
+// attention backward's dO image, then the MFMA attention backward of g (dq / dk / dv exactly as
+// attention_bwd writes them).  bf16, head size 64, d = 512, Lq, Lk <= 64.
+struct QkvBwd {
+  AttnGeom g;                 // as for attention_bwd (g.o_ld / o_bs unused: dO never leaves the launch)
+  const bf16* dA = nullptr;   // rows of image b at dA + (b * g.Lq + i) * ldda
+  int64_t ldda = 0;
+  const bf16* Wt = nullptr;   // Wo^T in the tiled layout (qkv_tile_weights_t)
+  bf16* dq = nullptr;
+  bf16* dk = nullptr;
+  bf16* dv = nullptr;
+};
+bool qkv_bwd_ok(const QkvBwd& a);
+void qkv_attn_bwd(const QkvBwd& a, hipStream_t s);
+// qkv_tile_weights of W^T for a 512 x 512 nn.Linear weight W [out][in] (row stride ld): dst holds
+// the [in][out] matrix tiled
+void qkv_tile_weights_t(const bf16* src, int64_t ld, bf16* dst, hipStream_t s);
+
 }  // namespace capgen

@@ -189,6 +189,122 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
   attn_fwd_staged(g, a.o, nullptr, b, h, sm);
 }
 
+// ---- the output side of the attention backward (QkvBwd) ----
+// Phase 0 as the cross front's projection (qkv_attn_kernel<LT, 1>): the image's dA rows staged in LDS,
+// wave w computes dO columns 16w .. 16w+15 of head h over every row with its 16 tiled Wo^T fragments
+// loaded in one batch; the bf16-rounded dO (the value a bf16 GEMM would store) goes to the dO image.
+// The K / Q / V rows are loaded into registers with the weights and written into their images only
+// after the projection, over the dA staging area (LDS: max(dA rows, 5 images) + the dO image).
+template <int LT>
+__global__ void __launch_bounds__(256) qkv_attn_bwd_kernel(QkvBwd a) {
+  constexpr int XS = LT * 16 * QD * 2;
+  constexpr int RA = XS > 5 * IMG ? XS : 5 * IMG;
+  __shared__ __attribute__((aligned(16))) char sm[RA + IMG + 64];
+  char* xs = sm;
+  char* Kimg = sm;
+  char* Qimg = sm + IMG;
+  char* Vimg = sm + 2 * IMG;
+  char* Pdimg = sm + 3 * IMG;
+  char* dSimg = sm + 4 * IMG;
+  char* dOimg = sm + RA;
+  unsigned char* kok = reinterpret_cast<unsigned char*>(sm + RA + IMG);
+  const AttnGeom& g = a.g;
+  StampScope stamp_scope(g.stamp);
+  if (g.prio) __builtin_amdgcn_s_setprio(3);
+  const int b = blockIdx.x / g.H, h = blockIdx.x % g.H;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+  const int L = g.Lq;
+  // every global load first: weights (16 tiled fragments), dA rows, K / Q / V rows, key flags
+  const bf16* wrow = a.Wt + ((int64_t)((h * DK + 16 * w) >> 4) * QKS * 64 + lane) * 8;
+  bf16x8 bq[QKS];
+#pragma unroll
+  for (int ks = 0; ks < QKS; ++ks) bq[ks] = *reinterpret_cast<const bf16x8*>(wrow + 512 * ks);
+  constexpr int CH = LT * 16 * QD / 8, PER = CH / 256;
+  const bf16* xb = a.dA + (int64_t)b * L * a.ldda;
+  uint4 xv[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int c = tid + 256 * u, row = c / (QD / 8), ch = c % (QD / 8);
+    xv[u] = *reinterpret_cast<const uint4*>(xb + (int64_t)min(row, L - 1) * a.ldda + ch * 8);
+  }
+  const int bk = g.kv_bmod ? b % g.kv_bmod : b;
+  const bf16* src[3] = {reinterpret_cast<const bf16*>(g.k) + (int64_t)bk * g.k_bs + h * DK,
+                        reinterpret_cast<const bf16*>(g.q) + (int64_t)b * g.q_bs + h * DK,
+                        reinterpret_cast<const bf16*>(g.v) + (int64_t)bk * g.v_bs + h * DK};
+  const int64_t ld[3] = {g.k_ld, g.q_ld, g.v_ld};
+  const int Ls[3] = {g.Lk, g.Lq, g.Lk};
+  uint4 kqv[3][2];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = tid + 256 * u, row = c >> 3, ch = c & 7;
+      kqv[i][u] = *reinterpret_cast<const uint4*>(src[i] + (int64_t)min(row, Ls[i] - 1) * ld[i] + ch * 8);
+    }
+  int kid = 0, kvl = 1;
+  if (w == 0) {
+    const int j = min(lane, g.Lk - 1);
+    kid = opaque(g.key_ids ? g.key_ids : g_qa_dummy)[g.key_ids ? (int64_t)b * g.kid_bs + j : lane];
+    kvl = opaque(g.key_valid ? g.key_valid : reinterpret_cast<const uint8_t*>(g_qa_dummy))[
+        g.key_valid ? (int64_t)bk * g.kv_bs + j : lane];
+  }
+  // dA rows -> LDS (rows >= L zero), the dO image zeroed (rows >= 16 LT are never projected)
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int c = tid + 256 * u, row = c / (QD / 8), ch = c % (QD / 8);
+    *reinterpret_cast<uint4*>(xs + row * (QD * 2) + xswz(row, ch) * 16) = row < L ? xv[u] : uint4{0u, 0u, 0u, 0u};
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) reinterpret_cast<uint4*>(dOimg)[tid + 256 * u] = uint4{0u, 0u, 0u, 0u};
+  __syncthreads();
+  f32x4 acc[LT];
+#pragma unroll
+  for (int i = 0; i < LT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < QKS; ++ks)
+#pragma unroll
+    for (int i = 0; i < LT; ++i) {
+      const int row = 16 * i + fr;
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(xs + row * (QD * 2) + xswz(row, 4 * ks + fg) * 16);
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[ks], af, acc[i], 0, 0, 0);
+    }
+  // lane holds dO[row 16i + fr][col 16w + 4fg + 0..3] (rows >= L: zero, from the zero dA rows)
+#pragma unroll
+  for (int i = 0; i < LT; ++i) {
+    const int row = 16 * i + fr, col = 16 * w + 4 * fg;
+    const bf16x4 r4 = {(bf16)acc[i][0], (bf16)acc[i][1], (bf16)acc[i][2], (bf16)acc[i][3]};
+    *reinterpret_cast<bf16x4*>(dOimg + row * 128 + swz(row, col >> 3) * 16 + (col & 7) * 2) = r4;
+  }
+  __syncthreads();  // (the dA staging area is free: K / Q / V images over it)
+  {
+    char* const img[3] = {Kimg, Qimg, Vimg};
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int c = tid + 256 * u, row = c >> 3, ch = c & 7;
+        *reinterpret_cast<uint4*>(img[i] + row * 128 + swz(row, ch) * 16) = row < Ls[i] ? kqv[i][u] : uint4{0u, 0u, 0u, 0u};
+      }
+    if (w == 0) kok[lane] = lane < g.Lk && (!g.key_valid || kvl != 0) && (!g.key_ids || kid != g.pad_idx);
+  }
+  __syncthreads();
+  attn_bwd_staged(g, a.dq, a.dk, a.dv, b, h, Kimg, dOimg, Qimg, Vimg, Pdimg, dSimg, kok);
+}
+
+__global__ void tile_weights_t_kernel(const bf16* __restrict__ src, int64_t ld, bf16* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // 16-B piece of dst (QD x QD)
+  if (i >= (int64_t)QD * QD / 8) return;
+  const int lane = (int)(i & 63), ks = (int)((i >> 6) % QKS);
+  const int64_t j = (i >> 6) / QKS;
+  const int64_t n = 16 * j + (lane & 15), k0 = 32 * ks + 8 * (lane >> 4);
+  bf16x8 v;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = src[(k0 + e) * ld + n];  // dst row n = column n of src
+  reinterpret_cast<bf16x8*>(dst)[i] = v;
+}
+
 __global__ void tile_weights_kernel(const bf16* __restrict__ src, int64_t n, int64_t ld, bf16* __restrict__ dst) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // 16-B piece of dst
   if (i >= n) return;
@@ -253,6 +369,50 @@ void qkv_attn_fwd(const QkvAttn& a, hipStream_t s) {
       default: qkv_attn_kernel<4, 3><<<grid, 256, 0, s>>>(a); break;
     }
   }
+  CAPGEN_HIP(hipGetLastError());
+}
+
+bool qkv_bwd_ok(const QkvBwd& a) {
+  const AttnGeom& g = a.g;
+  return g.dk == DK && g.H * DK == QD && g.Lq >= 1 && g.Lq <= 64 && g.Lk >= 1 && g.Lk <= 64 && !g.kv_row && a.Wt &&
+         a.dA && a.dq && a.dk && a.dv && a.ldda % 8 == 0 && g.q_ld % 8 == 0 && g.k_ld % 8 == 0 && g.v_ld % 8 == 0 &&
+         g.q_bs % 8 == 0 && g.k_bs % 8 == 0 && g.v_bs % 8 == 0;
+}
+
+void qkv_attn_bwd(const QkvBwd& a, hipStream_t s) {
+  require(qkv_bwd_ok(a), "qkv_attn_bwd: unsupported geometry (head size 64, d = 512, Lq / Lk <= 64)");
+  const AttnGeom& g = a.g;
+  if (hz::active()) {
+    using namespace hz;
+    const int Bk = g.kv_bmod > 0 ? std::min(g.B, g.kv_bmod) : g.B;
+    const int64_t w = (int64_t)g.H * g.dk;
+    const Rgn r[] = {rows_blk(a.dA, g.B, g.Lq, (int64_t)g.Lq * a.ldda, a.ldda, QD, 2, RD),
+                     rd(a.Wt, (int64_t)QD * QD * 2),
+                     rows_blk(g.q, g.B, g.Lq, g.q_bs, g.q_ld, w, 2, RD), rows_blk(g.k, Bk, g.Lk, g.k_bs, g.k_ld, w, 2, RD),
+                     rows_blk(g.v, Bk, g.Lk, g.v_bs, g.v_ld, w, 2, RD), blk(g.key_valid, Bk, g.Lk, g.kv_bs, RD),
+                     blk(g.key_ids, g.B, (int64_t)g.Lk * 4, g.kid_bs * 4, RD), rd(g.drop.seed_ptr, 8),
+                     rows_blk(a.dq, g.B, g.Lq, g.q_bs, g.q_ld, w, 2, WR),
+                     rows_blk(a.dk, Bk, g.Lk, g.k_bs, g.k_ld, w, 2, WR),
+                     rows_blk(a.dv, Bk, g.Lk, g.v_bs, g.v_ld, w, 2, WR)};
+    op(s, "qkv_attn_bwd", r, sizeof r / sizeof r[0]);
+  }
+  const dim3 grid(g.B * g.H);
+  switch ((g.Lq + 15) / 16) {
+    case 1: qkv_attn_bwd_kernel<1><<<grid, 256, 0, s>>>(a); break;
+    case 2: qkv_attn_bwd_kernel<2><<<grid, 256, 0, s>>>(a); break;
+    case 3: qkv_attn_bwd_kernel<3><<<grid, 256, 0, s>>>(a); break;
+    default: qkv_attn_bwd_kernel<4><<<grid, 256, 0, s>>>(a); break;
+  }
+  CAPGEN_HIP(hipGetLastError());
+}
+
+void qkv_tile_weights_t(const bf16* src, int64_t ld, bf16* dst, hipStream_t s) {
+  require(ld % 8 == 0 && ld >= QD, "qkv_tile_weights_t: ld >= 512");
+  if (hz::active()) {
+    using namespace hz;
+    hz::op(s, "qkv_tile_weights_t", {blk(src, QD, QD * 2, ld * 2, RD), wr(dst, (int64_t)QD * QD * 2)});
+  }
+  tile_weights_t_kernel<<<QD * QD / 8 / 256, 256, 0, s>>>(src, ld, dst);
   CAPGEN_HIP(hipGetLastError());
 }
 

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define CAPGEN_ABI_VERSION 7
+#define CAPGEN_ABI_VERSION 8
 
 typedef struct capgen_engine capgen_t;
 
@@ -223,6 +223,14 @@ int capgen_debug_qkv_attention(int B, int L, int H, const void* X, const void* W
  * key mask key_valid [B][Lk] (optional) into o [B*Lq, H*64].  Head size 64, H*64 = 512 only. */
 int capgen_debug_cross_attention(int B, int Lq, int Lk, int H, const void* X, const void* Wq, const void* KV, void* q,
                                  void* o, const unsigned char* key_valid, void* stream);
+
+/* Test hook: the fused output side of an attention block's backward (qkv_attn.hip qkv_attn_bwd;
+ * modules.py:77 o_linear + 16-27), bf16: dO = dA . Wo (dA [B*Lq, 512], Wo [512, 512] nn.Linear), then
+ * the masked attention backward over packed q [B*Lq, 512], k / v [B*Lk, 512] (key_valid [B][Lk]
+ * optional, causal) into dq / dk / dv.  Head size 64, H * 64 = 512. */
+int capgen_debug_attention_bwd_wo(int B, int Lq, int Lk, int H, const void* q, const void* k, const void* v,
+                                  const unsigned char* key_valid, int causal, const void* dA, const void* Wo, void* dq,
+                                  void* dk, void* dv, void* stream);
 
 /* Persisted GEMM autotune table (no reference counterpart: the reference's GEMMs are cuBLAS calls
  * of torch eager, models.py:120-126).  The bf16 GEMM picks a tile / wave / pipeline / split-K

@@ -933,6 +933,67 @@ def test_attention_kernels_vs_torch(dtype, B, H, Lq, Lk, dk, causal, mask):
         assert err < tol, (name, err)
 
 
+@pytest.mark.parametrize("B,Lq,Lk,mask", [(4, 36, 36, "valid"), (5, 19, 19, "causal"), (3, 19, 36, "valid"),
+                                          (64, 36, 36, "none"), (2, 64, 64, "causal"), (2, 1, 1, "none"),
+                                          (64, 19, 36, "valid")])
+def test_fused_attention_bwd_wo_vs_separate(B, Lq, Lk, mask):
+    """The output side of the attention backward in one launch (qkv_attn.hip qkv_attn_bwd: dO = dA . Wo
+    through the tiled Wo^T straight into the attention backward's LDS image) against the pair it
+    replaces -- the NN input-gradient GEMM, then the MFMA attention backward -- and against torch f32
+    autograd on the same bf16 inputs: dq / dk / dv within the bf16 attention-backward tolerance of
+    test_attention_kernels_vs_torch (3e-2 of the tensor's max), the two bf16 paths closer still (dO
+    differs by at most one rounding: the two MFMA paths sum k in different orders)."""
+    import ctypes as C
+    from capgen import _lib
+    lib = _lib.load()
+    H, d = 8, 512
+    g = torch.Generator(device="cpu").manual_seed(B * 7 + Lq * 3 + Lk)
+    q, k, v = ((torch.randn(B * L, d, generator=g) * 0.5).to(torch.bfloat16) for L in (Lq, Lk, Lk))
+    dA = (torch.randn(B * Lq, d, generator=g) * 0.5).to(torch.bfloat16)
+    Wo = (torch.randn(d, d, generator=g) / d ** 0.5).to(torch.bfloat16)
+    valid = torch.ones(B, Lk, dtype=torch.uint8)
+    if mask == "valid":
+        for b in range(B):
+            valid[b, max(1, Lk - 3 * b - 2):] = 0
+    causal = int(mask == "causal")
+    dev = lambda t: t.to(DEV).contiguous()
+    qd, kd, vd, dAd, Wod, vald = (dev(t) for t in (q, k, v, dA, Wo, valid))
+    ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None
+    out = []
+    for fused in (1, 0):
+        dq, dk, dv = (torch.zeros(B * L, d, device=DEV, dtype=torch.bfloat16) for L in (Lq, Lk, Lk))
+        if fused:
+            _lib.check(lib.capgen_debug_attention_bwd_wo(B, Lq, Lk, H, ptr(qd), ptr(kd), ptr(vd),
+                                                         ptr(vald) if mask == "valid" else None, causal, ptr(dAd),
+                                                         ptr(Wod), ptr(dq), ptr(dk), ptr(dv), None))
+        else:
+            dO = torch.empty(B * Lq, d, device=DEV, dtype=torch.bfloat16)
+            o = torch.empty(B * Lq, d, device=DEV, dtype=torch.bfloat16)
+            _lib.check(lib.capgen_debug_gemm(B * Lq, d, d, ptr(dAd), d, 0, ptr(Wod), d, 1, ptr(dO), d, 1, 1, None, 1.0,
+                                             0, 0, None))
+            _lib.check(lib.capgen_debug_attention(1, B, H, Lq, Lk, 64, ptr(qd), ptr(kd), ptr(vd),
+                                                  ptr(vald) if mask == "valid" else None, causal, 8.0, ptr(o), None,
+                                                  ptr(dO), ptr(dq), ptr(dk), ptr(dv), None))
+        torch.cuda.synchronize()
+        out.append([t.float().cpu() for t in (dq, dk, dv)])
+    # torch f32 reference on the bf16 inputs
+    qf, kf, vf = (t.float().view(B, L, H, 64).transpose(1, 2).requires_grad_(True) for t, L in ((q, Lq), (k, Lk), (v, Lk)))
+    s_ = (qf / 8.0) @ kf.transpose(-1, -2)
+    m = torch.zeros(B, 1, Lq, Lk, dtype=torch.bool)
+    if mask == "valid":
+        m = m | (valid[:, None, None, :] == 0)
+    if causal:
+        m = m | torch.triu(torch.ones(Lq, Lk, dtype=torch.bool), 1)[None, None]
+    o_ref = torch.softmax(s_.masked_fill(m, float("-inf")), -1) @ vf
+    dO_ref = (dA.float() @ Wo.float()).view(B, Lq, H, 64).transpose(1, 2)
+    o_ref.backward(dO_ref)
+    refs = [t.grad.transpose(1, 2).reshape(-1, d) for t in (qf, kf, vf)]
+    for (a1, a0, r) in zip(out[0], out[1], refs):
+        scale = r.abs().max().item() + 1e-12
+        assert (a1 - r).abs().max().item() / scale < 3e-2
+        assert (a1 - a0).abs().max().item() / scale < 2e-2
+
+
 @pytest.mark.parametrize("B,L,mask", [(4, 36, "none"), (3, 36, "valid_causal"), (5, 19, "ids_causal"), (2, 1, "none"),
                                        (2, 64, "valid_causal"), (3, 48, "ids_causal"), (64, 36, "none"),
                                        (4, 19, "cross36"), (3, 1, "cross36"), (64, 19, "cross36"), (2, 64, "cross64")])
@@ -1591,7 +1652,7 @@ def test_grouped_decode_attention_lds_staging_bit_identical(monkeypatch):
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("knob", ["CAPGEN_FUSED_QKV", "CAPGEN_DECODE_CROSS_MFMA"])
+@pytest.mark.parametrize("knob", ["CAPGEN_FUSED_QKV", "CAPGEN_DECODE_CROSS_MFMA", "CAPGEN_FUSED_ATTN_BWD"])
 def test_fused_attention_fronts_track_separate_launches_bf16(monkeypatch, knob):
     """The fused self / cross attention fronts (qkv_attn.hip; CAPGEN_FUSED_QKV, default on) against the
     GEMM + attention launches they replace, and the beam decode's cross attention on the MFMA attention
