@@ -21,7 +21,11 @@ OTHER = [(Me, d, 2176), (Md, d, d), (Me, 12 * d, d), (Md, V, d)]
 FRONT = [(Me, 3 * d, d)] * 6 + [(Md, 3 * d, d)] * 6 + [(Md, d, d)] * 5
 FWD = [(Me, d, d), (Me, f, d), (Me, d, f)] * 6 + [(Md, d, d), (Md, d, d), (Md, f, d), (Md, d, f)] * 6 + \
     [(Md, d, d)] + OTHER
-DX = ENC + DEC + OTHER[1:]
+# input gradients: the 18 output projections' (Wo, Wo_s, Wo_c) run inside the fused attention
+# backward (qkv_attn_bwd, round 4)
+WO_DX = [(Me, d, d)] * 6 + [(Md, d, d)] * 12
+DX = [(Me, 3 * d, d), (Me, f, d), (Me, d, f)] * 6 + [(Md, 3 * d, d), (Md, d, d), (Md, f, d), (Md, d, f)] * 6 + \
+    OTHER[1:]
 FWD_ALL = ENC + DEC + OTHER
 LN_ROWS = [Me] * 13 + [Md] * 19
 ALG = {  # class -> (GFLOP, algorithmic GB) per step
@@ -43,8 +47,10 @@ ALG = {  # class -> (GFLOP, algorithmic GB) per step
     # read q, k, v; write o  (self: rows x d each; cross: q/o over Md rows, k/v over Me rows)
     # (the one separate launch: decoder block 0's cross attention)
     "attention fwd": (0, (2 * Md + 2 * Me) * d * 2 / 1e9),
-    # read q, k, v, dO; write dq, dk, dv
-    "attention bwd": (0, (6 * 7 * Me * d * 2 + 6 * 7 * Md * d * 2 + 6 * (3 * Md + 4 * Me) * d * 2) / 1e9),
+    # fused: read dA, the Wo^T slice, q, k, v; write dq, dk, dv (dO never leaves the launch)
+    "attention bwd + Wo dX (fused)": (sum(2 * m * n * k for m, n, k in WO_DX) / 1e9,
+                                      (6 * 7 * Me * d * 2 + 6 * 7 * Md * d * 2 + 6 * (3 * Md + 4 * Me) * d * 2
+                                       + sum(n * k * 2 for m, n, k in WO_DX)) / 1e9),
     "Adam": (0, 30 * 55_707_408 / 1e9),
     "cross entropy": (0, (2 * Md * V * 2 + Md * ((V + 15) // 16) * 8) / 1e9),
 }
@@ -61,7 +67,8 @@ def klass(name):
             a = name.split("gemm_bf16_kernel<")[1].split(",")
             ta, tb = a[1].strip() == "true", a[2].strip() == "true"
         return "GEMM dW (TN)" if ta else "GEMM dX (NN)" if tb else "GEMM fwd (NT)"
-    for key, k in (("qkv_attn", "attention front (proj+attn)"), ("ln_fwd", "LayerNorm fwd"), ("ln_bwd", "LayerNorm bwd"), ("attn_fwd", "attention fwd"),
+    for key, k in (("qkv_attn_bwd", "attention bwd + Wo dX (fused)"), ("qkv_attn", "attention front (proj+attn)"),
+                   ("ln_fwd", "LayerNorm fwd"), ("ln_bwd", "LayerNorm bwd"), ("attn_fwd", "attention fwd"),
                    ("attn_bwd", "attention bwd"), ("adam_kernel", "Adam"), ("ce_finish", "cross entropy"),
                    ("ce_reg", "cross entropy")):
         if key in name:
