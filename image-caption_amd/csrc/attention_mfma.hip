@@ -33,6 +33,57 @@ __global__ void __launch_bounds__(256) attn_fwd_mfma_kernel(AttnGeom g, bf16* __
   attn_fwd_one(g, o, probs, blockIdx.x / g.H, blockIdx.x % g.H, sm);
 }
 
+// One wave64 per (batch, head) when every query row fits one 16-row tile (Lq <= 16: the beam's
+// cross attention at decode, an image's k beam rows over its keys).  The Q image holds only those
+// 16 rows: 2 + 8 + 8 KB + the key flags = 18.1 KB of LDS, so eight workgroups share a CU and the
+// decode's B * H = 2048 (image, head) pairs run in one round; the 4-wave kernel holds 24.6 KB
+// (six per CU, two rounds) and leaves three of its waves idle at Lq <= 16.  Same arithmetic as the
+// 4-wave kernel's wave 0 (attn_fwd_images): bit-identical results.
+__global__ void __launch_bounds__(64) attn_fwd_wave_kernel(AttnGeom g, bf16* __restrict__ o,
+                                                           float* __restrict__ probs) {
+  __shared__ __attribute__((aligned(16))) char sm[2 * IMG + 16 * 128 + 64];
+  StampScope stamp_scope(g.stamp);
+  if (g.prio) __builtin_amdgcn_s_setprio(3);
+  char* Kimg = sm;
+  char* Vimg = sm + IMG;
+  char* Qimg = sm + 2 * IMG;
+  unsigned char* kok = reinterpret_cast<unsigned char*>(sm + 2 * IMG + 16 * 128);
+  const int b = blockIdx.x / g.H, h = blockIdx.x % g.H, lane = threadIdx.x;
+  const int bk = g.kv_bmod ? b % g.kv_bmod : b;
+  const bf16* kb = reinterpret_cast<const bf16*>(g.k) + (int64_t)bk * g.k_bs + h * DK;
+  const bf16* vb = reinterpret_cast<const bf16*>(g.v) + (int64_t)bk * g.v_bs + h * DK;
+  const bf16* qb = reinterpret_cast<const bf16*>(g.q) + (int64_t)b * g.q_bs + h * DK;
+  // every load first (K / V: 64 rows x 8 chunks of 16 B, rows >= Lk zero; Q: 16 rows).  The loads
+  // of rows past Lk are skipped, not clamped: the kernel is bound by its load issue (clamped
+  // redundant loads of the last row measured 20.6 vs 9.4 us per launch at C4)
+  uint4 kv[2][8], qv[2];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int c = lane + 64 * u, row = c >> 3, ch = c & 7;
+    kv[0][u] = row < g.Lk ? *reinterpret_cast<const uint4*>(kb + (int64_t)row * g.k_ld + ch * 8) : uint4{0u, 0u, 0u, 0u};
+    kv[1][u] = row < g.Lk ? *reinterpret_cast<const uint4*>(vb + (int64_t)row * g.v_ld + ch * 8) : uint4{0u, 0u, 0u, 0u};
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = lane + 64 * u, row = c >> 3, ch = c & 7;
+    qv[u] = row < g.Lq ? *reinterpret_cast<const uint4*>(qb + (int64_t)row * g.q_ld + ch * 8) : uint4{0u, 0u, 0u, 0u};
+  }
+  stage_key_ok(kok, g, b, lane);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int c = lane + 64 * u, row = c >> 3, ch = c & 7;
+    *reinterpret_cast<uint4*>(Kimg + row * 128 + swz(row, ch) * 16) = kv[0][u];
+    *reinterpret_cast<uint4*>(Vimg + row * 128 + swz(row, ch) * 16) = kv[1][u];
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = lane + 64 * u, row = c >> 3, ch = c & 7;
+    *reinterpret_cast<uint4*>(Qimg + row * 128 + swz(row, ch) * 16) = qv[u];
+  }
+  __syncthreads();
+  attn_fwd_images(g, o, probs, b, h, Qimg, Kimg, Vimg, kok);
+}
+
 __global__ void __launch_bounds__(256) attn_bwd_mfma_kernel(AttnGeom g, const bf16* __restrict__ dout,
                                                             bf16* __restrict__ dq, bf16* __restrict__ dkp,
                                                             bf16* __restrict__ dvp) {
@@ -74,6 +125,15 @@ bool attention_mfma_ok(const AttnGeom& g) {
 }
 
 void attention_fwd_mfma(const AttnGeom& g, bf16* o, float* probs, hipStream_t s) {
+  // CAPGEN_ATTN_WAVE=0 (A/B + bit-identity test knob, read per launch: only Lq <= 16 asks)
+  if (g.Lq <= 16) {
+    const char* e = std::getenv("CAPGEN_ATTN_WAVE");
+    if (!e || e[0] != '0') {
+      attn_fwd_wave_kernel<<<g.B * g.H, 64, 0, s>>>(g, o, probs);
+      CAPGEN_HIP(hipGetLastError());
+      return;
+    }
+  }
   attn_fwd_mfma_kernel<<<g.B * g.H, 256, 0, s>>>(g, o, probs);
   CAPGEN_HIP(hipGetLastError());
 }

@@ -128,14 +128,12 @@ __device__ __forceinline__ void store4(bf16* p, f32x4 v, float mul) {
 }
 
 
-// forward of one (batch b, head h) once Q / K / V sit in the LDS images sm[0..3) and the key flags
-// after them (zero rows beyond Lq / Lk): S = Q K^T -> mask -> softmax -> [probs] -> dropout -> O = P V
-__device__ __forceinline__ void attn_fwd_staged(const AttnGeom& g, bf16* __restrict__ o, float* __restrict__ probs,
-                                                int b, int h, const char* sm) {
-  const char* Qimg = sm;
-  const char* Kimg = sm + IMG;
-  const char* Vimg = sm + 2 * IMG;
-  const unsigned char* kok = reinterpret_cast<const unsigned char*>(sm + 3 * IMG);
+// forward of one (batch b, head h) once Q / K / V sit in their LDS images and the key flags in kok
+// (zero rows beyond Lq / Lk; the Q image needs only this wave's 16 rows): S = Q K^T -> mask ->
+// softmax -> [probs] -> dropout -> O = P V.  Wave w takes query rows 16w .. 16w+15.
+__device__ __forceinline__ void attn_fwd_images(const AttnGeom& g, bf16* __restrict__ o, float* __restrict__ probs,
+                                                int b, int h, const char* Qimg, const char* Kimg, const char* Vimg,
+                                                const unsigned char* kok) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int q0 = 16 * w, q = q0 + (lane & 15);
   if (q0 >= g.Lq) return;
@@ -173,6 +171,12 @@ __device__ __forceinline__ void attn_fwd_staged(const AttnGeom& g, bf16* __restr
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_t(Vimg, 16 * t, 1, lane), pf1, acc, 0, 0, 0);
     if (q < g.Lq) store4(ob + (int64_t)q * g.o_ld + 16 * t + 4 * (lane >> 4), acc, 1.f);
   }
+}
+
+// the same with the images at sm[0..3) and the key flags after them
+__device__ __forceinline__ void attn_fwd_staged(const AttnGeom& g, bf16* __restrict__ o, float* __restrict__ probs,
+                                                int b, int h, const char* sm) {
+  attn_fwd_images(g, o, probs, b, h, sm, sm + IMG, sm + 2 * IMG, reinterpret_cast<const unsigned char*>(sm + 3 * IMG));
 }
 
 // forward of one (batch b, head h): 256 threads, sm = 3 [64][64] bf16 images + 64 key flags

@@ -885,6 +885,8 @@ def test_splitk_combine_bit_reproducible_under_load():
     (2, 4, 9, 9, 32, 1, True),      # C1 head size (VALU kernels in both dtypes)
     (5, 8, 1, 19, 64, 0, True),     # KV-cached decode step, self-attention length (attn_decode_kernel)
     (5, 8, 1, 36, 64, 0, True),     # KV-cached decode step over the regions (> 32 keys)
+    (5, 8, 5, 36, 64, 0, True),     # beam-5 cross attention at decode (one-wave kernel, Lq <= 16)
+    (3, 8, 16, 19, 64, 1, True),    # one full query tile, causal (one-wave kernel)
 ])
 def test_attention_kernels_vs_torch(dtype, B, H, Lq, Lk, dk, causal, mask):
     """ScaledDotProductAttention (modules.py:16-27) forward + backward through the C ABI vs a
@@ -931,6 +933,37 @@ def test_attention_kernels_vs_torch(dtype, B, H, Lq, Lk, dk, causal, mask):
         ref = ref.detach().float()
         err = (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-6)
         assert err < tol, (name, err)
+
+
+@pytest.mark.parametrize("B,Lq,Lk,causal,mask", [(5, 5, 36, 0, True), (4, 16, 36, 0, True), (3, 12, 19, 1, True),
+                                                  (2, 3, 64, 0, False), (256, 5, 36, 0, False)])
+def test_attention_one_wave_kernel_bit_identical(monkeypatch, B, Lq, Lk, causal, mask):
+    """The one-wave bf16 attention forward for Lq <= 16 (attention_mfma.hip attn_fwd_wave_kernel: the
+    beam's cross attention at decode) returns the same bits as the 4-wave kernel's wave 0
+    (CAPGEN_ATTN_WAVE=0), probabilities included."""
+    import ctypes as C
+    from capgen import _lib
+    lib = _lib.load()
+    H = 8
+    g = torch.Generator(device="cpu").manual_seed(B * 100 + Lq * 10 + Lk)
+    q, k, v = (torch.randn(B, L, H * 64, generator=g).to(torch.bfloat16).to(DEV) for L in (Lq, Lk, Lk))
+    valid = torch.ones(B, Lk, dtype=torch.uint8)
+    if mask:
+        for b in range(B):
+            valid[b, max(1, Lk - 3 * (b % 7) - 2):] = 0
+    vd = valid.to(DEV)
+    ptr = lambda t: C.c_void_p(t.data_ptr())
+    out = []
+    for wave in ("1", "0"):
+        monkeypatch.setenv("CAPGEN_ATTN_WAVE", wave)
+        o = torch.full_like(q, float("nan"))
+        probs = torch.full((B, H, Lq, Lk), float("nan"), device=DEV)
+        _lib.check(lib.capgen_debug_attention(1, B, H, Lq, Lk, 64, ptr(q), ptr(k), ptr(v), ptr(vd) if mask else None,
+                                              causal, 8.0, ptr(o), ptr(probs), None, None, None, None, None))
+        torch.cuda.synchronize()
+        out.append((o.cpu(), probs.cpu()))
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
 
 
 @pytest.mark.parametrize("B,Lq,Lk,mask", [(4, 36, 36, "valid"), (5, 19, 19, "causal"), (3, 19, 36, "valid"),
