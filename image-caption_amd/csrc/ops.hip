@@ -653,13 +653,15 @@ void cross_entropy_rows(const float* logits, const int32_t* tgt, int M, int V, i
 // workgroup per row: lse = M + log sum_c s_c exp(mx_c - M), loss_row = lse - v[tgt], and the
 // row is rewritten in place as softmax - onehot = e * exp(mx_c - lse) - onehot.  Every load of the
 // row (stats + the thread's slabs) is issued up front: one memory round trip.
-template <int SPT>
+template <int SPT, int VW>
 __global__ void __launch_bounds__(256) ce_finish_kernel(const float2* __restrict__ stats, int64_t ld,
                                                         const float* __restrict__ tlogit,
                                                         const int32_t* __restrict__ tgt, int V, int pad,
                                                         float* __restrict__ loss_row, bf16* __restrict__ dl) {
+  // VW = elements per access: 8 (16-B loads / stores, rows 16-B aligned: V % 8 == 0) or 4
   __shared__ float sh[4];
-  typedef __attribute__((ext_vector_type(4))) __bf16 b4;
+  typedef __attribute__((ext_vector_type(VW))) __bf16 bv;
+  constexpr int NQ = 16 / VW;  // accesses per 16-column slab
   const int m = blockIdx.x, nsl = (V + 15) / 16;
   bf16* row = dl + (int64_t)m * V;
   // every load first -- target, target logit, slab stats, the row's e values -- from clamped in-range
@@ -667,19 +669,19 @@ __global__ void __launch_bounds__(256) ce_finish_kernel(const float2* __restrict
   const int y = tgt[m];
   const float tl = tlogit[m];
   float2 st[SPT];
-  b4 e[SPT][4];
+  bv e[SPT][NQ];
 #pragma unroll
   for (int u = 0; u < SPT; ++u) {
     const int c = threadIdx.x + 256 * u, cc = min(c, nsl - 1);
     st[u] = stats[(int64_t)m * ld + cc];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) e[u][q] = *reinterpret_cast<const b4*>(row + min(cc * 16 + q * 4, V - 4));
+    for (int q = 0; q < NQ; ++q) e[u][q] = *reinterpret_cast<const bv*>(row + min(cc * 16 + q * VW, V - VW));
   }
 #pragma unroll
   for (int u = 0; u < SPT; ++u)
     if (threadIdx.x + 256 * u >= nsl) st[u] = float2{-INFINITY, 0.f};
   if (y == pad) {  // (uniform per workgroup)
-    for (int c = threadIdx.x * 4; c < V; c += 256 * 4) *reinterpret_cast<b4*>(row + c) = b4{0, 0, 0, 0};
+    for (int c = threadIdx.x * VW; c < V; c += 256 * VW) *reinterpret_cast<bv*>(row + c) = bv{};
     if (threadIdx.x == 0) loss_row[m] = 0.f;
     return;
   }
@@ -698,12 +700,17 @@ __global__ void __launch_bounds__(256) ce_finish_kernel(const float2* __restrict
     if (c >= nsl) continue;
     const float f = expf(st[u].x - lse);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int col = c * 16 + q * 4;
+    for (int q = 0; q < NQ; ++q) {
+      const int col = c * 16 + q * VW;
       if (col >= V) continue;
-      float o[4] = {(float)e[u][q][0] * f, (float)e[u][q][1] * f, (float)e[u][q][2] * f, (float)e[u][q][3] * f};
-      if (y >= col && y < col + 4) o[y - col] -= 1.f;
-      *reinterpret_cast<b4*>(row + col) = b4{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+      bv o;
+#pragma unroll
+      for (int i = 0; i < VW; ++i) {
+        float x = (float)e[u][q][i] * f;
+        if (y == col + i) x -= 1.f;
+        o[i] = (bf16)x;
+      }
+      *reinterpret_cast<bv*>(row + col) = o;
     }
   }
   if (threadIdx.x == 0) loss_row[m] = lse - tl;
@@ -718,11 +725,20 @@ void ce_finish(const float2* stats, int64_t ld, const float* tlogit, const int32
                         rd(tgt, (int64_t)M * 4), wr(loss_row, (int64_t)M * 4), wr(dl, (int64_t)M * V * 2)});
   }
   const int spt = ((V + 15) / 16 + 255) / 256;
-  if (spt <= 1) ce_finish_kernel<1><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl);
-  else if (spt <= 2) ce_finish_kernel<2><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl);
-  else if (spt <= 3) ce_finish_kernel<3><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl);
-  else if (spt <= 4) ce_finish_kernel<4><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl);
-  else if (spt <= 8) ce_finish_kernel<8><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl);
+  // 16-B accesses when every row starts 16-B aligned (CAPGEN_CE_VEC8=0: the 8-B form -- A/B and
+  // bit-identity test knob, read per launch: one launch per step)
+  const char* ve = std::getenv("CAPGEN_CE_VEC8");
+  const bool v8 = !(ve && ve[0] == '0') && V % 8 == 0 && ((uintptr_t)dl & 15) == 0;
+  auto go = [&](auto spt_c) {
+    constexpr int S = decltype(spt_c)::value;
+    if (v8) ce_finish_kernel<S, 8><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl);
+    else ce_finish_kernel<S, 4><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl);
+  };
+  if (spt <= 1) go(std::integral_constant<int, 1>{});
+  else if (spt <= 2) go(std::integral_constant<int, 2>{});
+  else if (spt <= 3) go(std::integral_constant<int, 3>{});
+  else if (spt <= 4) go(std::integral_constant<int, 4>{});
+  else if (spt <= 8) go(std::integral_constant<int, 8>{});
   else throw Error("ce_finish: V > 32768");
   CAPGEN_HIP(hipGetLastError());
 }

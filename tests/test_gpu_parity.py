@@ -1685,6 +1685,29 @@ def test_grouped_decode_attention_lds_staging_bit_identical(monkeypatch):
     assert torch.equal(a, b)
 
 
+def test_ce_finish_16b_accesses_bit_identical(monkeypatch):
+    """ce_finish (the fused classifier + CE's second half, ops.hip) with 16-B row accesses gives the
+    same loss and Linear weight gradients, bit for bit, as its 8-B form (CAPGEN_CE_VEC8=0): bf16 C2
+    step.  (LayerNorm / bias sums and the word-embedding scatter use f32 atomics, whose order varies
+    run to run: those to 1e-4, as in test_bf16_weight_gradients_bit_reproducible.)"""
+    out = []
+    for v in ("1", "0"):
+        monkeypatch.setenv("CAPGEN_CE_VEC8", v)
+        _, cfg, sd, e, f, p, c = _c2_setup(dtype="bf16", weights="fixture")
+        e.set_training(False)
+        loss = e.forward(f.to(DEV).bfloat16(), p.to(DEV), c.to(DEV)).item()
+        e.backward()
+        torch.cuda.synchronize()
+        out.append((loss, e.grads_state_dict()))
+    assert out[0][0] == out[1][0]
+    for n in out[0][1]:
+        a, b = out[0][1][n], out[1][1][n]
+        if a.dim() == 2 and n != "decoder.word_embedding.weight":
+            assert torch.equal(a, b), n
+        else:
+            assert torch.allclose(a, b, rtol=1e-4, atol=1e-7 * a.abs().max().item()), n
+
+
 @pytest.mark.parametrize("knob", ["CAPGEN_FUSED_QKV", "CAPGEN_DECODE_CROSS_MFMA", "CAPGEN_FUSED_ATTN_BWD"])
 def test_fused_attention_fronts_track_separate_launches_bf16(monkeypatch, knob):
     """The fused self / cross attention fronts (qkv_attn.hip; CAPGEN_FUSED_QKV, default on) against the
