@@ -22,6 +22,8 @@
 //   * the f32 results are rounded to bf16 once -- exactly the values a bf16 GEMM store would leave
 //     in the qkv buffer -- and written to the buffer and to the three [64][64] LDS images;
 //   * then attn_fwd_staged (attention_mfma.hip's forward body) runs on the images.
+#include <cstdlib>
+
 #include "qkv_attn.h"
 
 #include "attn_mfma_dev.h"
@@ -87,7 +89,8 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int c = tid + 256 * u, row = c / (QD / 8), ch = c % (QD / 8);
-      v[u] = *reinterpret_cast<const uint4*>(xb + (int64_t)min(row, L - 1) * a.ldx + ch * 8);
+      v[u] = row < L || a.clamp ? *reinterpret_cast<const uint4*>(xb + (int64_t)min(row, L - 1) * a.ldx + ch * 8)
+                                : uint4{0u, 0u, 0u, 0u};
     }
     // cross attention: K / V head slices from memory (rows < Lk, clamped, unconditional)
     uint4 kv[2][2];
@@ -101,7 +104,9 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const int c = tid + 256 * u, row = c >> 3, ch = c & 7;
-          kv[i][u] = *reinterpret_cast<const uint4*>(src[i] + (int64_t)min(row, g.Lk - 1) * ld[i] + ch * 8);
+          kv[i][u] = row < g.Lk || a.clamp
+                         ? *reinterpret_cast<const uint4*>(src[i] + (int64_t)min(row, g.Lk - 1) * ld[i] + ch * 8)
+                         : uint4{0u, 0u, 0u, 0u};
         }
     }
     // key flags (stage_key_ok's two dependent conditional loads, as one unconditional batch)
@@ -227,7 +232,8 @@ __global__ void __launch_bounds__(256) qkv_attn_bwd_kernel(QkvBwd a) {
 #pragma unroll
   for (int u = 0; u < PER; ++u) {
     const int c = tid + 256 * u, row = c / (QD / 8), ch = c % (QD / 8);
-    xv[u] = *reinterpret_cast<const uint4*>(xb + (int64_t)min(row, L - 1) * a.ldda + ch * 8);
+    xv[u] = row < L || a.clamp ? *reinterpret_cast<const uint4*>(xb + (int64_t)min(row, L - 1) * a.ldda + ch * 8)
+                               : uint4{0u, 0u, 0u, 0u};
   }
   const int bk = g.kv_bmod ? b % g.kv_bmod : b;
   const bf16* src[3] = {reinterpret_cast<const bf16*>(g.k) + (int64_t)bk * g.k_bs + h * DK,
@@ -241,7 +247,9 @@ __global__ void __launch_bounds__(256) qkv_attn_bwd_kernel(QkvBwd a) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int c = tid + 256 * u, row = c >> 3, ch = c & 7;
-      kqv[i][u] = *reinterpret_cast<const uint4*>(src[i] + (int64_t)min(row, Ls[i] - 1) * ld[i] + ch * 8);
+      kqv[i][u] = row < Ls[i] || a.clamp
+                      ? *reinterpret_cast<const uint4*>(src[i] + (int64_t)min(row, Ls[i] - 1) * ld[i] + ch * 8)
+                      : uint4{0u, 0u, 0u, 0u};
     }
   int kid = 0, kvl = 1;
   if (w == 0) {
@@ -336,7 +344,18 @@ bool qkv_attn_ok(const QkvAttn& a) {
          a.ldx % 8 == 0 && a.ldqkv % 8 == 0 && g.o_ld % 8 == 0 && g.o_bs % 8 == 0;
 }
 
-void qkv_attn_fwd(const QkvAttn& a, hipStream_t s) {
+// CAPGEN_QKV_CLAMP=1 (A/B knob): load the staged rows past L / Lk from the last row instead of skipping them
+static int qkv_clamp() {
+  static const int c = [] {
+    const char* e = std::getenv("CAPGEN_QKV_CLAMP");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return c;
+}
+
+void qkv_attn_fwd(const QkvAttn& a_in, hipStream_t s) {
+  QkvAttn a = a_in;
+  a.clamp = qkv_clamp();
   require(qkv_attn_ok(a), "qkv_attn_fwd: unsupported geometry (head size 64, d = 512, self attention, L <= 64)");
   const AttnGeom& g = a.g;
   if (hz::active()) {
@@ -379,7 +398,9 @@ bool qkv_bwd_ok(const QkvBwd& a) {
          g.q_bs % 8 == 0 && g.k_bs % 8 == 0 && g.v_bs % 8 == 0;
 }
 
-void qkv_attn_bwd(const QkvBwd& a, hipStream_t s) {
+void qkv_attn_bwd(const QkvBwd& a_in, hipStream_t s) {
+  QkvBwd a = a_in;
+  a.clamp = qkv_clamp();
   require(qkv_bwd_ok(a), "qkv_attn_bwd: unsupported geometry (head size 64, d = 512, Lq / Lk <= 64)");
   const AttnGeom& g = a.g;
   if (hz::active()) {
