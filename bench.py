@@ -46,13 +46,16 @@ def dominant_class(eng, args, steps=3):
     of a train step records the GPU's 100 MHz real-time counter at its first workgroup's start and its
     last workgroup's end (capgen_debug_stamps, no profiler); run `steps` stamped steps after the timed
     region, group the launches by class, and price the class with the largest summed time per step
-    (the NN input-gradient GEMMs at C2) at its algorithmic FLOPs / its average launch duration."""
+    (the NN input-gradient GEMMs at C2) at its algorithmic FLOPs / its summed launch durations -- only when
+    every launch of the class ran on one stream (launches on different streams overlap, and their summed
+    durations would overstate the class's time).  Runs train steps: call it after every measurement that
+    needs the engine's state."""
     from collections import defaultdict
     eng.stamps(1)
     for _ in range(2):
         eng.train_step_raw(*args)
     torch.cuda.synchronize()
-    cls = defaultdict(lambda: [0, 0.0, 0.0])  # launches, us, flops
+    cls = defaultdict(lambda: [0, 0.0, 0.0, set()])  # launches, us, flops, streams
     for _ in range(steps):
         eng.stamps(3)
         eng.train_step_raw(*args)
@@ -61,7 +64,9 @@ def dominant_class(eng, args, steps=3):
             if t1 <= 0 or t0 <= 0 or t1 < t0:
                 continue
             words = name.split()  # "<stream> gemm dX MxNxK" / "<stream> ln_bwd M" / ...
-            kind = " ".join(words[1:3]) if words[1] == "gemm" else words[1]
+            if len(words) < 2:
+                continue
+            kind = " ".join(words[1:3]) if words[1] == "gemm" and len(words) >= 3 else words[1]
             fl = 0.0
             if words[1] == "gemm" and "x" in words[-1]:
                 m, n_, k = (int(x) for x in words[-1].split("x"))
@@ -70,12 +75,14 @@ def dominant_class(eng, args, steps=3):
             c[0] += 1
             c[1] += t1 - t0
             c[2] += fl
+            c[3].add(words[0])
     eng.stamps(0)
-    kind, (n, us, fl) = max(cls.items(), key=lambda kv: kv[1][1])
+    kind, (n, us, fl, streams) = max(cls.items(), key=lambda kv: kv[1][1])
     avg_us = us / n
-    tf = fl / (us * 1e-6) / 1e12 if fl else None
+    tf = fl / (us * 1e-6) / 1e12 if fl and len(streams) == 1 else None
     names = {"gemm dX": "gemm_bf16_kernel NN input-gradient GEMMs (dX = dY . W)", "gemm fwd": "gemm_bf16_kernel NT forward GEMMs"}
     return {"kernel": names.get(kind, kind) + ", in-step class (stamped launches: first workgroup start -> last workgroup end)",
+            "streams": sorted(streams),
             "launches_per_step": round(n / steps, 1), "us_per_step": round(us / steps, 1), "avg_us": round(avg_us, 2),
             "achieved": round(tf, 1) if tf else None, "unit": "TFLOP/s",
             "frac": round(tf / PEAK_BF16_TFLOPS, 4) if tf else None,
@@ -226,6 +233,21 @@ def main():
         elapsed = t.item()
     final_loss = loss.item()
     step_ms_events = ev0.elapsed_time(ev1) / args.steps
+    # correctness of a data-parallel run (after the timed region): the communicator the engine's
+    # collectives ran on, parameters bit-identical on every rank (exact checksum, min == max over the
+    # ranks), every rank holding the same global loss (model.py:76's mean over the global batch)
+    comm_n, _ = eng.dp_comm_info()
+    dp = {"rccl_ranks": comm_n if comm_n else 1, "engine_communicator": bool(comm_n)}
+    if world > 1:
+        ck = eng.params_checksum()
+        ck = ck - (1 << 64) if ck >= (1 << 63) else ck
+        t = torch.tensor([ck, -ck], device=dev, dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        lt = torch.tensor([final_loss, -final_loss], device=dev, dtype=torch.float64)
+        dist.all_reduce(lt, op=dist.ReduceOp.MAX)
+        dp["params_equal_across_ranks"] = bool(t[0].item() == -t[1].item())
+        dp["global_loss"] = round(final_loss, 6)
+        dp["loss_equal_across_ranks"] = bool(lt[0].item() == -lt[1].item())
 
     images = B * world * args.steps
     value = images / elapsed
@@ -251,14 +273,16 @@ def main():
                                                          f"summary {traffic['source']} (not measured in this run)"
                                                          if traffic else "")},
         "final_loss": round(final_loss, 5),
+        "dp_check": dp,
         # diagnostic: host enqueue time per step; close to ms_per_step means the host issue rate,
         # not the GPU, sets the step time
         "host_issue_ms_per_step": round(issue_s / args.steps * 1e3, 4),
     }
     if rank == 0 and world == 1:
-        out["dominant_kernel"] = dominant_class(eng, (f, ft, p, c, B, N, T, loss))
         if not args.no_host_batches:
             out["host_batches"] = host_batches(eng, cfg, dev)
+        # (runs stamped train steps: after everything else that uses the engine)
+        out["dominant_kernel"] = dominant_class(eng, (f, ft, p, c, B, N, T, loss))
         if not args.no_cpu_baseline:
             del eng
             torch.cuda.empty_cache()

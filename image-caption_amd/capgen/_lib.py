@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CAPGEN_LIB_PATH") or os.path.join(_HERE, "libcapgen.so")  # (diagnostic builds)
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 F32, BF16 = 0, 1
 
@@ -45,6 +45,8 @@ _P = C.c_void_p
 _SIGS = {
     "capgen_last_error": (C.c_char_p, []),
     "capgen_abi_version": (C.c_int, []),
+    "capgen_set_knob": (C.c_int, [C.c_char_p, C.c_int, _P]),
+    "capgen_debug_build": (C.c_int, []),
     "capgen_param_table": (C.c_int, [C.POINTER(capgen_config), C.POINTER(capgen_param_info), C.c_int,
                                      C.POINTER(C.c_int), C.POINTER(C.c_int64)]),
     "capgen_create": (C.c_int, [C.POINTER(capgen_config), C.c_int, C.POINTER(_P)]),
@@ -89,6 +91,8 @@ _SIGS = {
     "capgen_dp_init": (C.c_int, [_P, C.c_char_p, C.c_int, C.c_int]),
     "capgen_dp_set_global_count": (C.c_int, [_P, C.c_float]),
     "capgen_dp_sync_adam_state": (C.c_int, [_P]),
+    "capgen_dp_comm_info": (C.c_int, [_P, _P, _P]),
+    "capgen_params_checksum": (C.c_int, [_P, _P]),
     "capgen_dp_buckets": (C.c_int, [_P, _P, _P, C.c_int, _P]),
     "capgen_dp_debug_shard": (C.c_int, [_P, C.c_int, C.c_int]),
     "capgen_tune_load": (C.c_int, [C.c_char_p]),
@@ -206,3 +210,15 @@ def hazard_check(cap: int = 8192):
 def side_delay(us: float) -> None:
     """Spin `us` microseconds in front of every launch off the critical stream (0 = off)."""
     check(load().capgen_debug_side_delay(float(us)))
+
+
+def set_knob(name: str, value: int) -> int:
+    """Set a run-time switch (capgen_set_knob; name without the CAPGEN_ prefix); returns the old value."""
+    old = C.c_int(0)
+    check(load().capgen_set_knob(name.encode(), int(value), C.byref(old)))
+    return old.value
+
+
+def debug_build() -> bool:
+    """True in the debug library (libcapgen_debug.so, CAPGEN_LIB_PATH)."""
+    return bool(load().capgen_debug_build())

@@ -25,9 +25,13 @@ def broadcast_unique_id(uid: bytes | None, rank: int) -> bytes:
     return obj[0]
 
 
-def init_engine_dp(engine, rank: int, world: int):
-    from .engine import Engine
-    uid = Engine.dp_unique_id() if rank == 0 else None
+def init_engine_dp(engine, rank: int, world: int, unique_id=None):
+    """Bootstrap the engine's communicator: rank 0 makes the RCCL unique id (`unique_id`, default
+    Engine.dp_unique_id), the process group carries it to every rank, every rank calls dp_init."""
+    if unique_id is None:
+        from .engine import Engine
+        unique_id = Engine.dp_unique_id
+    uid = unique_id() if rank == 0 else None
     uid = broadcast_unique_id(uid, rank) if world > 1 else uid
     engine.dp_init(uid, rank, world)
 

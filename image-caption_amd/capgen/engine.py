@@ -276,6 +276,18 @@ class Engine:
         assert len(uid) == 128
         _lib.check(self.lib.capgen_dp_init(self.h, uid, rank, world))
 
+    def dp_comm_info(self):
+        """(communicator size, this rank) of the engine's RCCL communicator; (0, 0) before dp_init."""
+        n, r = C.c_int(0), C.c_int(0)
+        _lib.check(self.lib.capgen_dp_comm_info(self.h, C.byref(n), C.byref(r)))
+        return n.value, r.value
+
+    def params_checksum(self) -> int:
+        """Exact, order-independent checksum of the f32 parameters (equal on every rank of a DP run)."""
+        v = C.c_uint64(0)
+        _lib.check(self.lib.capgen_params_checksum(self.h, C.byref(v)))
+        return v.value
+
     def dp_set_global_count(self, count: float):
         _lib.check(self.lib.capgen_dp_set_global_count(self.h, float(count)))
 

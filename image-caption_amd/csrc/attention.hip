@@ -517,8 +517,7 @@ static void launch_decode(const AttnGeom& g, T* o, float* probs, hipStream_t s) 
       // (round 3): 1 wave 14.7-15.7 ms/batch, 2 waves 14.2-14.5, 4 waves 14.6-14.7, 8 waves 15.1-15.2
       // (one wave per beam row, round 2: 25.1 vs 18.8 us/launch)
       const int nt = grouped ? 128 : 256;
-      const char* kv_env = std::getenv("CAPGEN_DECODE_GROUP_LDS");  // (read per launch: tests toggle it)
-      const int kv_lds = kv_env && kv_env[0] == '0' ? 0 : 1;
+      const int kv_lds = knob(Knob::DecodeGroupLds) ? 1 : 0;
       const int lds = grouped ? kv_lds : 0;
       if (g.Lk <= 24) attn_decode_bf16_kernel<3><<<blocks, nt, 0, s>>>(g, Gk, o, probs, lds);
       else if (g.Lk <= 40) attn_decode_bf16_kernel<5><<<blocks, nt, 0, s>>>(g, Gk, o, probs, lds);

@@ -119,16 +119,14 @@ __global__ void __launch_bounds__(256) attn_bwd_mfma_kernel(AttnGeom g, const bf
 }
 
 bool attention_mfma_ok(const AttnGeom& g) {
-  static const bool off = std::getenv("CAPGEN_ATTN_VALU") != nullptr;  // A/B experiment knob
-  return !off && g.dk == DK && g.Lq <= 64 && g.Lk <= 64 && g.q_ld % 8 == 0 && g.k_ld % 8 == 0 && g.v_ld % 8 == 0 &&
+  return g.dk == DK && g.Lq <= 64 && g.Lk <= 64 && g.q_ld % 8 == 0 && g.k_ld % 8 == 0 && g.v_ld % 8 == 0 &&
          g.o_ld % 8 == 0 && g.q_bs % 8 == 0 && g.k_bs % 8 == 0 && g.v_bs % 8 == 0 && g.o_bs % 8 == 0;
 }
 
 void attention_fwd_mfma(const AttnGeom& g, bf16* o, float* probs, hipStream_t s) {
-  // CAPGEN_ATTN_WAVE=0 (A/B + bit-identity test knob, read per launch: only Lq <= 16 asks)
+  // Knob::AttnWave = 0: the 4-wave kernel (bit-identity test)
   if (g.Lq <= 16) {
-    const char* e = std::getenv("CAPGEN_ATTN_WAVE");
-    if (!e || e[0] != '0') {
+    if (knob(Knob::AttnWave)) {
       attn_fwd_wave_kernel<<<g.B * g.H, 64, 0, s>>>(g, o, probs);
       CAPGEN_HIP(hipGetLastError());
       return;

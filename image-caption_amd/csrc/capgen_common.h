@@ -5,6 +5,8 @@
 #include <stdint.h>
 #include <string>
 
+#include "capgen_host.h"
+
 typedef __bf16 bf16;
 
 #define CAPGEN_HIP(expr)                                                                  \
@@ -17,20 +19,16 @@ typedef __bf16 bf16;
 
 namespace capgen {
 
-struct Error {
-  std::string msg;
-  explicit Error(std::string m) : msg(std::move(m)) {}
-};
-
-inline void require(bool ok, const std::string& what) {
-  if (!ok) throw Error(what);
+// Debug build only (Knob::Skip bitmask): skip a kernel class to measure its marginal cost on the
+// step's critical path.  1 LN fwd, 2 attention fwd, 4 LN bwd, 8 attention bwd, 16 GEMM f32-out
+// (weight gradients + classifier), 32 Adam, 64 bf16 GEMMs, 128 LayerNorm-backward gamma/beta/bias sums.
+inline int skip_mask() {
+#ifdef CAPGEN_DEBUG
+  return knob(Knob::Skip);
+#else
+  return 0;
+#endif
 }
-
-// Diagnostic only (CAPGEN_SKIP bitmask, never set in production): skip a kernel class to
-// measure its marginal cost on the step's critical path.  1 LN fwd, 2 attention fwd, 4 LN bwd,
-// 8 attention bwd, 16 GEMM f32-out (weight gradients + classifier), 32 Adam, 64 bf16 GEMMs,
-// 128 LayerNorm-backward gamma/beta/bias sums.
-int skip_mask();
 
 // ---- diagnostic in-kernel timestamps (capgen_debug_stamps) --------------------------------
 // A launch given a stamp slot (16 x u64) records the 100 MHz real-time counter: [0] when block 0
@@ -70,15 +68,9 @@ __device__ __forceinline__ void wt_store16(__amdgpu_buffer_rsrc_t r, uint32_t of
 // N consecutive elements of T at byte offset `off` from the rsrc base (16-B pieces), write-through
 template <typename T, int N>
 __device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, uint32_t off, const float (&in)[N]);
-// write-through default: off (CAPGEN_WT=1 enables; measured slower in the step, 4-round A/B 3.16-3.22
-// vs 3.04-3.17 ms: the end-of-launch write-back is not what the ~3 us kernel boundary is made of)
-inline int wt_default() {
-  static const int on = [] {
-    const char* e = std::getenv("CAPGEN_WT");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
+// write-through default: off (measured slower in the step, 4-round A/B 3.16-3.22 vs 3.04-3.17 ms: the
+// end-of-launch write-back is not what the ~3 us kernel boundary is made of); callers may set wt = 1
+inline int wt_default() { return 0; }
 
 // ---- scalar conversions -------------------------------------------------------------
 // (store_wt after the conversions below)

@@ -207,10 +207,12 @@ struct capgen_engine {
     for (auto& w : ws) tiled[w.first] = {n, w.second}, n += (int64_t)std::abs(w.second) * 512;
     if (n) CAPGEN_HIP(hipMalloc(&wtile, (size_t)n * 2));
   }
-  // re-tile the fronts' weights inside the arena range [off, off + n) from the shadow
+  // re-tile the fronts' weights that overlap the arena range [off, off + n) from the shadow (a matrix
+  // cut by a range boundary is re-tiled by both ranges' calls; the later one, on the same stream, sees
+  // the whole matrix updated)
   void retile(int64_t off, int64_t n, hipStream_t s, bool trans_only = false) {
     for (auto& kv : tiled)
-      if (kv.first >= off && kv.first < off + n) {
+      if (kv.first < off + n && kv.first + (int64_t)std::abs(kv.second.second) * 512 > off) {
         if (kv.second.second < 0) qkv_tile_weights_t(shadow + kv.first, 512, wtile + kv.second.first, s);
         else if (!trans_only) qkv_tile_weights(shadow + kv.first, kv.second.second, 512, wtile + kv.second.first, s);
       }
@@ -225,10 +227,7 @@ struct capgen_engine {
   static constexpr int NSTRIPE = 16;
   float* gstripe = nullptr;
   bool stripes_dirty = true;  // gstripe may hold partials (the next backward zeroes it first)
-  bool stripe_clear = [] {    // the folds zero the partials they read (CAPGEN_STRIPE_CLEAR=0: memset per step)
-    const char* e = std::getenv("CAPGEN_STRIPE_CLEAR");
-    return !(e && e[0] == '0');
-  }();
+  bool stripe_clear = knob(Knob::StripeClear) != 0;  // the folds zero the partials they read (0: memset per step)
   int64_t n_small = 0;
   bool training = true;
   bool fwd_drop = true;  // dropout state of the last forward (backward must match)
@@ -244,10 +243,7 @@ struct capgen_engine {
   bool graph_on = false;
   hipGraphExec_t gexec = nullptr;
   // eager step mode: the forward alone as a linear graph (CAPGEN_FWD_GRAPH=0 disables)
-  bool fwd_graph_on = [] {
-    const char* e = std::getenv("CAPGEN_FWD_GRAPH");
-    return !(e && e[0] == '0');
-  }();
+  bool fwd_graph_on = knob(Knob::FwdGraph) != 0;
   hipGraphExec_t fexec = nullptr;
   // split forward graphs (CAPGEN_FWD_SPLIT=1, with the decoder front on es2): the front and the
   // critical chain as separate LINEAR graphs on their own streams.  Under rocprofv3 the one
@@ -258,10 +254,7 @@ struct capgen_engine {
   // step also issues the per-bucket collectives.  The single graph is the default at every world
   // size (faster on the GPU; the count / partial-CE all-reduces capture into it as well);
   // CAPGEN_FWD_SPLIT=1 selects the split graphs
-  int fwd_split_env = [] {
-    const char* e = std::getenv("CAPGEN_FWD_SPLIT");
-    return e ? (e[0] == '1' ? 1 : 0) : -1;
-  }();
+  int fwd_split_env = knob(Knob::FwdSplit);
   bool fwd_split() const { return fwd_split_env == 1; }
   bool cap_split = false;  // forward() is being captured in split mode: it ends/begins captures
   hipGraph_t fg[4] = {};   // pre, front, encoder, decoder
@@ -314,10 +307,7 @@ struct capgen_engine {
   // shadow of the bucket re-cast locally.  Same bytes over xGMI as the all-reduce (RS + AG), 1/world
   // of the 1.67 GB Adam stream.  CAPGEN_ZERO=0: all-reduce + full Adam on every rank;
   // CAPGEN_ZERO=2: the sharded code path even at world 1 (RCCL test hook).
-  int zero_mode = [] {
-    const char* e = std::getenv("CAPGEN_ZERO");
-    return e ? std::atoi(e) : 1;
-  }();
+  int zero_mode = knob(Knob::Zero);
   int zemu_rank = 0, zemu_world = 1;  // capgen_dp_debug_shard: shard as rank r of w, no collectives
   // set by the sharded update: the Adam moments (resp. the gradient arena) are current in this rank's
   // chunks only until capgen_dp_sync_adam_state (resp. the next backward) -- the whole-arena getters
@@ -359,28 +349,19 @@ struct capgen_engine {
 
   // issue priority of a launch: kernels on the critical stream run their waves at s_setprio 3 so
   // that the weight-gradient / Adam waves of the side streams sharing their CUs yield the issue
-  // slots to them (CAPGEN_PRIO=0 disables)
-  bool prio_on = [] {
-    const char* e = std::getenv("CAPGEN_PRIO");
-    return !(e && e[0] == '0');
-  }();
+  // slots to them (measured 2.779 / 2.788 vs 2.782 / 2.795 ms/step without, round 4)
+  static constexpr bool prio_on = true;
   hipStream_t crit = nullptr;  // critical stream of the running call (es, or the caller's: direct)
   int prio(hipStream_t s) const { return prio_on && s == (crit ? crit : es) && es2 != s ? 1 : 0; }
-  // direct steps (CAPGEN_DIRECT, default on): once the forward graph exists, train_step runs its
+  // direct steps: once the forward graph exists, train_step runs its
   // critical path on the CALLER's stream -- no caller -> engine -> caller event round trip per
   // step; es then waits for the step so the engine's host-side syncs on es still cover it
   // (measured: 3.165 vs 3.170 ms/step, within noise -- the step-boundary gap is the Adam tail)
   // fused classifier + cross entropy in the bf16 path (CAPGEN_FUSED_CE=0: logits in f32 + ce_kernel)
-  bool fused_ce_on = [] {
-    const char* e = std::getenv("CAPGEN_FUSED_CE");
-    return !(e && e[0] == '0');
-  }();
+  bool fused_ce_on = knob(Knob::FusedCe) != 0;
   bool need_logits = false;  // the next forward must materialise the f32 logits (SCST sampling)
   bool fused_ce() const { return fused_ce_on && !need_logits && act == DType::BF16 && L_().V % 4 == 0; }
-  bool direct_on = [] {
-    const char* e = std::getenv("CAPGEN_DIRECT");
-    return !(e && e[0] == '0');
-  }();
+  static constexpr bool direct_on = true;
 
   // diagnostic in-kernel timestamps (capgen_debug_stamps): every GEMM / LayerNorm / attention
   // launch of a step gets a slot of the ring (forward slots first: a captured forward graph keeps
@@ -430,10 +411,7 @@ struct capgen_engine {
   // (qkv_attn.hip: projection straight into the attention's LDS images; qkv still written for the
   // backward).  Otherwise (f32 parity mode, other geometries, CAPGEN_FUSED_QKV=0) the GEMM and the
   // attention launch.
-  bool fused_qkv_on = [] {
-    const char* e = std::getenv("CAPGEN_FUSED_QKV");
-    return !(e && e[0] == '0');
-  }();
+  bool fused_qkv_on = knob(Knob::FusedQkv) != 0;
   void self_attention(const void* X, int64_t wqkv, int M, int d, const AttnGeom& g, void* qkv, void* att, float* probs,
                       hipStream_t s) {
     if (fused_qkv_on && act == DType::BF16 && !keep_probs(g)) {
@@ -734,10 +712,7 @@ struct capgen_engine {
   };
   // off by default: measured slower than eager issue on MI355X / ROCm 7 (C4 B=256: beam 5
   // 22.6 vs 21.9 ms, greedy 12.4 vs 11.6 ms, tools/bench_generate.py); CAPGEN_GEN_GRAPH=1 enables
-  bool gen_graph_on = [] {
-    const char* e = std::getenv("CAPGEN_GEN_GRAPH");
-    return e && e[0] == '1';
-  }();
+  bool gen_graph_on = knob(Knob::GenGraph) == 1;
   static constexpr size_t kGenGraphs = 8;  // cached decode graphs (oldest evicted)
   std::vector<std::pair<GenKey, hipGraphExec_t>> gen_graphs;
   std::vector<GenKey> gen_seen;  // keys run eagerly once (next call captures)
@@ -1034,10 +1009,7 @@ struct capgen_engine {
   }
   // hazard-checker self-test (CAPGEN_DEBUG_DROP_JOIN=1): the side stream is never joined back --
   // a deliberately missing edge the checker must report (results are then racy: test use only)
-  bool dbg_drop_join = [] {
-    const char* e = std::getenv("CAPGEN_DEBUG_DROP_JOIN");
-    return e && e[0] == '1';
-  }();
+  bool dbg_drop_join = knob(Knob::DebugDropJoin) == 1;  // (debug build only)
   // Weight-gradient GEMMs are queued and issued on es2 in one batch per block (flush): an event
   // record/wait pair costs the recording stream ~7 us of bubble on ROCm 7 (tools/kprobe.hip:
   // 13 us per eager fork/join pair), so the critical stream records one event per block instead
@@ -1050,10 +1022,7 @@ struct capgen_engine {
     const float* alpha_ptr;
   };
   std::vector<DwJob> dw_pending;
-  bool group_dw = [] {  // CAPGEN_GROUP_DW=0: one launch per weight (A/B experiments, tests)
-    const char* e = std::getenv("CAPGEN_GROUP_DW");
-    return !(e && e[0] == '0');
-  }();
+  bool group_dw = knob(Knob::GroupDw) != 0;  // 0: one launch per weight (tests)
   void dw_side(const void* dY, int64_t ldy, const void* X, int64_t ldx, int64_t goff, int64_t ldg, int M, int N,
                int K, const float* alpha_ptr, hipStream_t s) {
     if (es2 == s) {
@@ -1094,10 +1063,7 @@ struct capgen_engine {
     float* db;
   };
   std::vector<ColJob> col_pending;
-  bool colsum_side = [] {
-    const char* e = std::getenv("CAPGEN_COLSUM_SIDE");
-    return !(e && e[0] == '0');
-  }();
+  bool colsum_side = knob(Knob::ColsumSide) != 0;
   // es2 waits for everything issued on s so far, then runs the queued weight-gradient GEMMs
   void flush(hipStream_t s) {
     fork(s);
@@ -1110,14 +1076,8 @@ struct capgen_engine {
   // with the encoder chain: once block 0's cross-attention backward has produced its K/V
   // gradient, the encoder-output gradient (all blocks' gKV . Wkv_all) is complete, and nothing
   // the encoder backward reads depends on the rest of block 0 (CAPGEN_OVERLAP_DEC0=0: serial)
-  bool overlap_front = [] {  // CAPGEN_OVERLAP_FRONT=0: the decoder front runs after the encoder
-    const char* e = std::getenv("CAPGEN_OVERLAP_FRONT");
-    return !(e && e[0] == '0');
-  }();
-  bool overlap_dec0 = [] {
-    const char* e = std::getenv("CAPGEN_OVERLAP_DEC0");
-    return !(e && e[0] == '0');
-  }();
+  bool overlap_front = knob(Knob::OverlapFront) != 0;  // 0: the decoder front runs after the encoder
+  bool overlap_dec0 = knob(Knob::OverlapDec0) != 0;
   // GemmArgs of dX[M,K] (+)= dY[M,N] . W[N,K] (linear_dx) without launching it
   GemmArgs dx_args(const void* dY, int64_t ldy, int64_t woff, int64_t ldw, void* dX, int64_t ldx, int M, int N,
                    int K, int beta) const {
@@ -1151,10 +1111,7 @@ struct capgen_engine {
   // gradient (dO = dA . Wo, dA = lb.d_a) runs INSIDE the attention backward launch (qkv_attn_bwd):
   // one launch and one dependent boundary fewer per attention block (CAPGEN_FUSED_ATTN_BWD=0: the
   // dX GEMM into gATT and the attention backward launch)
-  bool fused_attn_bwd_on = [] {
-    const char* e = std::getenv("CAPGEN_FUSED_ATTN_BWD");
-    return !(e && e[0] == '0');
-  }();
+  bool fused_attn_bwd_on = knob(Knob::FusedAttnBwd) != 0;
   void mha_bwd(int M, int d, const LnBwd& lb, const void* att, int64_t Wo, void* gATT, const AttnGeom& g,
                const float* probs, void* dq, void* dk, void* dv, hipStream_t s) {
     if (fused_attn_bwd_on && act == DType::BF16 && WTo(Wo) && attention_mfma_ok(g)) {
@@ -1181,8 +1138,10 @@ struct capgen_engine {
     AdamTiles at;
     bool fused_tiles = true;
     for (auto& kv : tiled)
-      if (ns > 0 && kv.second.second > 0 && kv.first >= off && kv.first < off + ns) {
-        if (at.n == AdamTiles::kMax) {
+      if (ns > 0 && kv.second.second > 0 && kv.first < off + ns && kv.first + (int64_t)kv.second.second * 512 > off) {
+        // a tiled matrix only partly inside this range (a bucket boundary through it): re-tile after
+        if (at.n == AdamTiles::kMax || kv.first < off || kv.first + (int64_t)kv.second.second * 512 > off + ns ||
+            (kv.first - off) % 4 != 0) {
           fused_tiles = false;
           break;
         }
@@ -1209,10 +1168,7 @@ struct capgen_engine {
   // from_s: every producer of the bucket's gradients ran on s (no flush, ec waits for s)
   bool bstep = false;
   // transformer blocks per gradient bucket (one flush = one event record on the critical stream)
-  int bucket_blocks = [] {
-    const char* e = std::getenv("CAPGEN_BUCKET_BLOCKS");
-    return e ? std::max(1, std::atoi(e)) : 1;
-  }();
+  int bucket_blocks = std::max(1, knob(Knob::BucketBlocks));
   void bucket(int64_t off, int64_t n, hipStream_t s, bool sync = true, bool from_s = false) {
     if (sync && !from_s) flush(s);
     if (!bstep) return;
@@ -1543,6 +1499,36 @@ struct capgen_engine {
     hz::wait(cs, ev_out);
   }
 
+  // Once, after the first train step at world > 1: every rank must hold the same GLOBAL non-pad count
+  // (the count all-reduce inside the forward -- captured in its graph -- gives the reference's mean over
+  // the global batch, model.py:76) and so the same loss.  Max and min over the ranks of both, one
+  // grouped 4-value exchange; a mismatch fails the step (non-zero status, capgen_last_error).
+  bool dp_checked = false;
+  float* dp_chk = nullptr;  // [4] device scratch: count max, count min, loss max, loss min
+  void dp_check(hipStream_t cs, const float* loss) {
+    if (dp_checked || !comm || world <= 1) return;
+    dp_checked = true;
+    if (!dp_chk) CAPGEN_HIP(hipMalloc(&dp_chk, 4 * sizeof(float)));
+    for (int i = 0; i < 2; ++i) {
+      CAPGEN_HIP(hipMemcpyAsync(dp_chk + i, a.count, sizeof(float), hipMemcpyDeviceToDevice, cs));
+      CAPGEN_HIP(hipMemcpyAsync(dp_chk + 2 + i, loss ? loss : a.count, sizeof(float), hipMemcpyDeviceToDevice, cs));
+    }
+    NCCL_CHECK(ncclGroupStart());
+    NCCL_CHECK(ncclAllReduce(dp_chk, dp_chk, 1, ncclFloat, ncclMax, comm, cs));
+    NCCL_CHECK(ncclAllReduce(dp_chk + 1, dp_chk + 1, 1, ncclFloat, ncclMin, comm, cs));
+    NCCL_CHECK(ncclAllReduce(dp_chk + 2, dp_chk + 2, 1, ncclFloat, ncclMax, comm, cs));
+    NCCL_CHECK(ncclAllReduce(dp_chk + 3, dp_chk + 3, 1, ncclFloat, ncclMin, comm, cs));
+    NCCL_CHECK(ncclGroupEnd());
+    float hv[4];
+    CAPGEN_HIP(hipMemcpyAsync(hv, dp_chk, sizeof hv, hipMemcpyDeviceToHost, cs));
+    CAPGEN_HIP(hipStreamSynchronize(cs));
+    require(hv[0] == hv[1] && hv[0] > 0.f,
+            "dp: the global target count differs across ranks after the first step (max " + std::to_string(hv[0]) +
+                ", min " + std::to_string(hv[1]) + ")");
+    require(hv[2] == hv[3], "dp: the global loss differs across ranks after the first step (max " +
+                                std::to_string(hv[2]) + ", min " + std::to_string(hv[3]) + ")");
+  }
+
   void train_step(const void* f, DType ft, const float* pos, const int32_t* caps, int B, int N, int T, float* loss,
                   hipStream_t cs) {
     ensure_acts(B, N, T);
@@ -1562,7 +1548,7 @@ struct capgen_engine {
     }
     enter(cs);
     auto body = [&]() {
-      static const bool host_timing = std::getenv("CAPGEN_HOST_TIMING") != nullptr;  // diagnostic
+      const bool host_timing = knob(Knob::HostTiming) != 0;  // (debug build)
       static double tf = 0, tb = 0;
       static int nsteps = 0;
       auto t0 = std::chrono::steady_clock::now();
@@ -1623,7 +1609,7 @@ struct capgen_engine {
         }
         fkey = k;
       }
-      static const bool host_timing = std::getenv("CAPGEN_HOST_TIMING") != nullptr;  // diagnostic
+      const bool host_timing = knob(Knob::HostTiming) != 0;  // (debug build)
       static double tb = 0, tl = 0;
       static int nsteps = 0;
       auto t0 = std::chrono::steady_clock::now();
@@ -1900,16 +1886,10 @@ struct capgen_engine {
   }
   // bf16 beam decode: the cross attention of an image's beam rows on the MFMA attention kernel
   // (CAPGEN_DECODE_CROSS_MFMA=0: the grouped VALU decode kernel, attention.hip)
-  bool cross_mfma_on = [] {
-    const char* e = std::getenv("CAPGEN_DECODE_CROSS_MFMA");
-    return !(e && e[0] == '0');
-  }();
+  bool cross_mfma_on = knob(Knob::DecodeCrossMfma) != 0;
   // bf16 decode: the classifier epilogue writes slab stats and the greedy / beam selection reads
   // k * 16 logits per row instead of the whole row (CAPGEN_SLAB_DECODE=0: full-row kernels)
-  bool slab_decode_on = [] {
-    const char* e = std::getenv("CAPGEN_SLAB_DECODE");
-    return !(e && e[0] == '0');
-  }();
+  bool slab_decode_on = knob(Knob::SlabDecode) != 0;
   bool slab_decode() const { return slab_decode_on && act == DType::BF16 && L.V % 4 == 0 && slab_select_ok(L.V); }
 
   void greedy(const void* feats, DType ft, const float* pos, int B, int N, int64_t* ids_out, float* attn_out,
@@ -2004,6 +1984,7 @@ struct capgen_engine {
                     (void*)adam_scal, (void*)seed, (void*)scalars, (void*)gstripe, ws, gws, (void*)stamp_ring})
       if (p) (void)hipFree(p);
     if (count_host) (void)hipHostFree(count_host);
+    if (dp_chk) (void)hipFree(dp_chk);
     if (ev_in) (void)hipEventDestroy(ev_in);
     if (ev_out) (void)hipEventDestroy(ev_out);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
@@ -2069,6 +2050,17 @@ extern "C" {
 const char* capgen_last_error(void) { return g_last_error.c_str(); }
 int capgen_abi_version(void) { return CAPGEN_ABI_VERSION; }
 
+int capgen_set_knob(const char* name, int value, int* old) {
+  return guarded([&] {
+    require(name != nullptr, "set_knob: null name");
+    const int rc = knob_set(name, value, old);
+    require(rc != -1, std::string("set_knob: unknown switch ") + name);
+    require(rc != -2, std::string("set_knob: ") + name + " exists only in the debug build (libcapgen_debug.so)");
+  });
+}
+
+int capgen_debug_build(void) { return debug_build() ? 1 : 0; }
+
 int capgen_param_table(const capgen_config* cfg, capgen_param_info* out, int cap, int* count, int64_t* arena_elems) {
   return guarded([&] {
     require(cfg != nullptr, "null config");
@@ -2099,8 +2091,7 @@ int capgen_create(const capgen_config* cfg, int device, capgen_t** out) {
     CAPGEN_HIP(hipStreamCreateWithFlags(&h->es, hipStreamNonBlocking));
     // CAPGEN_STREAMS (experiment knob): 3 = critical path + weight-grad + bucket streams
     // (default), 2 = buckets on the weight-grad stream, 1 = everything on one stream
-    const char* ns_env = std::getenv("CAPGEN_STREAMS");
-    const int nstreams = ns_env ? std::atoi(ns_env) : 3;
+    const int nstreams = knob(Knob::Streams);
     if (nstreams >= 2) CAPGEN_HIP(hipStreamCreateWithFlags(&h->es2, hipStreamNonBlocking));
     else h->es2 = h->es;
     // the fork / join / bucket events only order this device's own streams, so they skip the
@@ -2108,8 +2099,7 @@ int capgen_create(const capgen_config* cfg, int device, capgen_t** out) {
     // invalidates L2 around every record / wait; the kernels' own device-scope fences order the
     // streams).  Measured, three alternating runs each: 2.760-2.776 ms/step vs 2.817-2.838 with the
     // system fence, 2.815-2.832 with a device-scope release only (CAPGEN_EVENT_FENCE = 1 / 0 / 2).
-    const char* ef_env = std::getenv("CAPGEN_EVENT_FENCE");
-    const int ef = ef_env ? std::atoi(ef_env) : 1;
+    const int ef = knob(Knob::EventFence);
     const unsigned evf = hipEventDisableTiming | (ef == 1 ? hipEventDisableSystemFence : ef == 2 ? hipEventReleaseToDevice : 0u);
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_fork, evf));
     CAPGEN_HIP(hipEventCreateWithFlags(&h->ev_join, evf));
@@ -2297,6 +2287,7 @@ int capgen_train_step(capgen_t* h, const void* feats, int ft, const float* pos, 
   return guarded([&] {
     set_device(h);
     h->train_step(feats, dt(ft), pos, caps, B, N, T, loss_out, (hipStream_t)stream);
+    h->dp_check((hipStream_t)stream, loss_out);
   });
 }
 
@@ -2686,6 +2677,28 @@ int capgen_dp_init(capgen_t* h, const char id[128], int rank, int world) {
     NCCL_CHECK(ncclBroadcast(h->params, h->params, (size_t)h->L.total, ncclFloat, 0, h->comm, h->es));
     h->refresh_shadow(h->es);
     hz::host_sync(h->es);
+  });
+}
+
+int capgen_dp_comm_info(capgen_t* h, int* nranks, int* rank) {
+  return guarded([&] {
+    int n = 0, r = 0;
+    if (h->comm) {
+      NCCL_CHECK(ncclCommCount(h->comm, &n));
+      NCCL_CHECK(ncclCommUserRank(h->comm, &r));
+    }
+    if (nranks) *nranks = n;
+    if (rank) *rank = r;
+  });
+}
+
+int capgen_params_checksum(capgen_t* h, uint64_t* out) {
+  return guarded([&] {
+    set_device(h);
+    require(out != nullptr, "params_checksum: null output");
+    hz::host_sync(h->es);
+    hz::host_sync(h->ec);
+    *out = arena_checksum(h->params, (size_t)h->L.total, h->es);
   });
 }
 

@@ -122,25 +122,32 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs g) {
   lb.store(Bs[0], tid);
   __syncthreads();
 
-  // f32 operands: blocked accumulation -- each 256-deep K panel is summed in `acc`, then added into
-  // `tot` (a two-level sum like a CPU sgemm's K blocking: ~K/256 + 64 chained roundings per output
-  // instead of K/4; at K = 2304 the single chain was ~5x further from the float64 result than the
-  // reference's CPU arithmetic on the cancelling random-init weight gradients)
-  constexpr int KPANEL = 256 / BK;
-  f32x4 tot[FM][FN];
+  // f32 operands: three-level blocked accumulation -- each 64-deep K panel is summed in `acc` (a
+  // 64-fma chain), four panels in `mid`, and the 256-deep sums in `tot`: ~64 + 4 + K/256 chained
+  // roundings per output instead of K (a single chain at K = 2304 was ~5x further from the float64
+  // result than the reference's CPU arithmetic on the cancelling random-init weight gradients; one
+  // 256-deep level left encoder block 0's FFN-up gradient at ~3x the CPU's error, round 4)
+  constexpr int KP1 = 64 / BK, KP2 = 4;
+  f32x4 mid[FM][FN], tot[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) tot[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FN; ++j) mid[i][j] = tot[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, fq = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if constexpr (sizeof(T) == 4) {
-      if (kt > 0 && kt % KPANEL == 0) {
+      if (kt > 0 && kt % KP1 == 0) {
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < FN; ++j) tot[i][j] += acc[i][j], acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int j = 0; j < FN; ++j) mid[i][j] += acc[i][j], acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (kt % (KP1 * KP2) == 0) {
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) tot[i][j] += mid[i][j], mid[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
       }
     }
     if (kt + 1 < nk) {
@@ -183,11 +190,11 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs g) {
   }
 
   if constexpr (sizeof(T) == 4) {
-    if (nk > KPANEL) {
+    if (nk > KP1) {  // (K <= 64: the chain alone)
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] += tot[i][j];
+        for (int j = 0; j < FN; ++j) acc[i][j] = tot[i][j] + (mid[i][j] + acc[i][j]);
     }
   }
   // ---- epilogue ----
@@ -262,10 +269,9 @@ void gemm_hz_regions(const GemmArgs& g, DType in, DType out, bool ta, bool tb, s
 }
 
 static void gemm_impl(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t s);
-// CAPGEN_HOST_TIMING (diagnostic): average host time of a gemm() call, printed every 2000 calls
+// debug build, Knob::HostTiming: average host time of a gemm() call, printed every 2000 calls
 void gemm(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t s) {
-  static const bool timing = std::getenv("CAPGEN_HOST_TIMING") != nullptr;
-  if (!timing) return gemm_impl(g, in, out, ta, tb, s);
+  if (!knob(Knob::HostTiming)) return gemm_impl(g, in, out, ta, tb, s);
   static double tot = 0;
   static long n = 0;
   const auto t0 = std::chrono::steady_clock::now();

@@ -43,6 +43,7 @@
 #include "gemm.h"
 #include "hazard.h"
 #include "gemm_tile.h"
+#include "tune_parse.h"
 
 namespace capgen {
 
@@ -126,10 +127,7 @@ std::map<hipStream_t, Workspace> g_ws;
 // split-K hand-off protocol (diagnostic; 0 = production, see gemm_tile): bit 0 writer release,
 // bit 1 no reader acquire, bit 2 sc1 slab loads, bit 3 per-launch ticket memset, bit 4 ticket
 // re-armed by a relaxed atomic store (round 1: 2|4|16)
-int g_splitk_proto = [] {
-  const char* e = std::getenv("CAPGEN_SPLITK_PROTO");
-  return e ? std::atoi(e) : 0;
-}();
+int g_splitk_proto = 0;  // (debug build: Knob::SplitkProto, read at gemm_init)
 std::mutex g_ws_mu;
 uint64_t* g_timing_buf = nullptr;  // ablation build, protocol bit 4096 (gemm_set_timing_buf)
 
@@ -185,12 +183,8 @@ static void launch_cfg(const GemmArgs& g, hipStream_t s, int splitk) {
     if (g_splitk_proto & 8) CAPGEN_HIP(hipMemsetAsync(cnt, 0, (size_t)(tn * tm + 3) / 4 * 16, s));
   }
   // group_m ~ sqrt(tiles per XCD), so each XCD's tile block is about square
-  static const bool grouping = [] {
-    const char* e = std::getenv("CAPGEN_GEMM_GROUP");
-    return !(e && e[0] == '0');
-  }();
   int group_m = 0;
-  if (grouping) {
+  {
     const double per_xcd = (double)tn * tm / 8.0;
     group_m = std::max(1, std::min(tm, (int)std::lround(std::sqrt(per_xcd))));
   }
@@ -238,11 +232,7 @@ constexpr int kVariantKG[NVARIANTS + 1] = {0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1
 // written by exactly one workgroup.  CAPGEN_ALLOW_PARTIAL_LINES=1 lifts the rule (diagnostic).
 template <typename TO>
 static bool whole_lines(int v) {
-  static const bool allow = [] {
-    const char* e = std::getenv("CAPGEN_ALLOW_PARTIAL_LINES");
-    return e && e[0] == '1';
-  }();
-  return allow || kVariantBN[v] * (int)sizeof(TO) >= 128;
+  return knob(Knob::AllowPartialLines) || kVariantBN[v] * (int)sizeof(TO) >= 128;
 }
 
 template <typename TO, bool TA, bool TB>
@@ -302,39 +292,19 @@ std::mutex g_tune_mu;
 int g_live_tuned = 0;  // shapes (plain + grouped) tuned live in this process
 
 bool autotune_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("CAPGEN_AUTOTUNE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+  return knob(Knob::Autotune) != 0;
 }
 
 // Tuning-time clock of one (variant, split-K) candidate: 3 launches.  In the step every GEMM
 // reads operands that are not in this XCD's L2 (the A operand was just written by the previous
 // kernel -- possibly on another XCD -- and the weights were last touched a step ago), so the
 // latency-bound small shapes run ~2x their L2-warm repeat time there (dec W2 1216x512x2048:
-// 24.6 us in the step, 11.9 us repeated).  With CAPGEN_TUNE_COLD (default on) each timed launch
-// follows a 64 MB scrub write that evicts the L2s, so the tuner ranks candidates under the
-// step's cache state; the scrub itself is outside the timed span.
-static bool tune_cold() {
-  static const bool on = [] {
-    const char* e = std::getenv("CAPGEN_TUNE_COLD");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+// 24.6 us in the step, 11.9 us repeated).  So each timed launch follows a 64 MB scrub write that
+// evicts the L2s, and the tuner ranks candidates under the step's cache state (the warm repeat
+// clock measured 3.236 vs 2.977 ms/step); the scrub itself is outside the timed span.
 template <typename F>
 static float tune_time(F&& launch, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   launch();  // warm-up (code, TLB)
-  if (!tune_cold()) {
-    CAPGEN_HIP(hipEventRecord(e0, s));
-    for (int r = 0; r < 3; ++r) launch();
-    CAPGEN_HIP(hipEventRecord(e1, s));
-    CAPGEN_HIP(hipEventSynchronize(e1));
-    float ms = 0.f;
-    CAPGEN_HIP(hipEventElapsedTime(&ms, e0, e1));
-    return ms;
-  }
   static std::map<int, void*> scrub;  // per device, never freed (tuning-time helper)
   constexpr size_t kScrub = 64u << 20;
   int dev = 0;
@@ -374,14 +344,11 @@ static Choice tune(const GemmArgs& g, hipStream_t s) {
   Choice best{heuristic_variant(g), 1};
   float best_ms = 1e30f;
   const int nk = (g.K + BK - 1) / BK;
-  // split-K factor cap (CAPGEN_MAX_SPLITK, default 8).  Round 1 capped it at 2 because the bf16
+  // split-K factor cap 8.  Round 1 capped it at 2 because the bf16
   // step was not reproducible run to run with higher factors; the causes were a sub-line output
   // tile under a read-modify-write epilogue (whole_lines) and the combine's ticket re-arm /
   // missing acquire (gemm_tile) -- tools/step_det_probe.py: 0 of 60 diverging runs at cap 8 now.
-  static const int max_sk = [] {
-    const char* e = std::getenv("CAPGEN_MAX_SPLITK");
-    return e ? std::max(1, std::atoi(e)) : 8;
-  }();
+  constexpr int max_sk = 8;
   for (int sk : {1, 2, 3, 4, 6, 8}) {
     if (sk > max_sk || (sk > 1 && nk < 4 * sk)) break;
     if (sk > 1) ensure_ws(s, splitk_bytes(g, sk));
@@ -394,7 +361,7 @@ static Choice tune(const GemmArgs& g, hipStream_t s) {
   CAPGEN_HIP(hipEventDestroy(e0));
   CAPGEN_HIP(hipEventDestroy(e1));
   CAPGEN_HIP(hipFree(scratch));
-  if (std::getenv("CAPGEN_AUTOTUNE_LOG"))
+  if (knob(Knob::AutotuneLog))
     std::fprintf(stderr, "[capgen gemm] M=%d N=%d K=%d ta=%d tb=%d out=%s -> %s splitk=%d (%.2f us)\n", g.M, g.N, g.K,
                  TA, TB, sizeof(TO) == 4 ? "f32" : "bf16", kVariantName[best.variant], best.splitk,
                  best_ms * 1e3f / 3);
@@ -404,18 +371,15 @@ static Choice tune(const GemmArgs& g, hipStream_t s) {
 template <typename TO, bool TA, bool TB>
 static void launch_bf16_tiles(const GemmArgs& g, hipStream_t s) {
   Choice c{g_variant % 100, std::max(1, g_variant / 100)};  // forced: variant + 100 * splitk
-  if (TA && c.variant == 0) {  // experiment knob: weight-gradient (TN) GEMMs on a fixed variant
-    static const int dwv = [] {
-      const char* e = std::getenv("CAPGEN_DW_VARIANT");
-      return e ? std::atoi(e) : 0;
-    }();
+  if (TA && c.variant == 0) {  // debug build: weight-gradient (TN) GEMMs on a fixed variant
+    const int dwv = knob(Knob::DwVariant);
     if (dwv) c = Choice{dwv % 100, std::max(1, dwv / 100)};
   }
-  // experiment knob: CAPGEN_GEMM_FORCE="M,N,K,ta,tb,v[;...]" pins one shape's choice (variant v +
+  // debug build: CAPGEN_GEMM_FORCE="M,N,K,ta,tb,v[;...]" pins one shape's choice (variant v +
   // 100 * split-K), e.g. to A/B a critical-path GEMM in the step rather than alone
   static const std::map<TuneKey, int> forced = [] {
     std::map<TuneKey, int> m;
-    if (const char* e = std::getenv("CAPGEN_GEMM_FORCE")) {
+    if (const char* e = debug_build() ? std::getenv("CAPGEN_GEMM_FORCE") : nullptr) {
       int M, N, K, ta, tb, v, n = 0;
       for (const char* p = e; *p;) {
         if (std::sscanf(p, "%d,%d,%d,%d,%d,%d%n", &M, &N, &K, &ta, &tb, &v, &n) != 6) break;
@@ -489,11 +453,6 @@ GroupTable g_group_table[64];
 std::mutex g_group_table_mu;
 
 const GemmGroup* grouped_args_dev(const GemmGroup& gg, int dev, hipStream_t s) {
-  static const bool on = [] {
-    const char* e = std::getenv("CAPGEN_GROUP_ARGS_DEV");
-    return !(e && e[0] == '0');
-  }();
-  if (!on) return nullptr;
   const unsigned char* b = reinterpret_cast<const unsigned char*>(&gg);
   uint64_t h = 1469598103934665603ull;
   for (size_t i = 0; i < sizeof(GemmGroup); ++i) h = (h ^ b[i]) * 1099511628211ull;
@@ -530,10 +489,8 @@ static void launch_group_cfg(const GemmArgs* ps, int n, hipStream_t s) {
   // the grouped (weight-gradient) grid is capped at one workgroup per CU, each looping over its
   // tiles: the side-stream dW work then leaves room on every CU for the critical stream's
   // latency-bound kernels (step 3.44-3.47 vs 3.54 ms uncapped; 64 workgroups: 3.75 ms, the dW
-  // work becomes critical).  CAPGEN_DW_GRID overrides (0 = uncapped).
+  // work becomes critical; round 4 re-sweep: 256 vs 192 / 320 / 128, tools/r04_dwgrid.sh).
   static const int cap = [] {
-    const char* e = std::getenv("CAPGEN_DW_GRID");
-    if (e) return std::atoi(e) / 8 * 8;
     int n = 0, dev = 0;
     CAPGEN_HIP(hipGetDevice(&dev));
     CAPGEN_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
@@ -606,7 +563,7 @@ static void launch_group(const GemmArgs* ps, int n, hipStream_t s) {
         for (void* p : scratch) CAPGEN_HIP(hipFree(p));
         CAPGEN_HIP(hipStreamSynchronize(s));
         g_group_tuned[key] = v;
-        if (std::getenv("CAPGEN_AUTOTUNE_LOG"))
+        if (knob(Knob::AutotuneLog))
           std::fprintf(stderr, "[capgen gemm] group of %d (M=%d N=%d K=%d first) -> %s (%.2f us)\n", n, ps[0].M,
                        ps[0].N, ps[0].K, kVariantName[v], best * 1e3f / 3);
       }
@@ -616,10 +573,9 @@ static void launch_group(const GemmArgs* ps, int n, hipStream_t s) {
 }
 
 static void gemm_grouped_impl(const GemmArgs* ps, int n, DType out, bool ta, bool tb, hipStream_t s);
-// CAPGEN_HOST_TIMING (diagnostic): average host time of a grouped launch, printed every 500 calls
+// debug build, Knob::HostTiming: average host time of a grouped launch, printed every 500 calls
 void gemm_grouped(const GemmArgs* ps, int n, DType out, bool ta, bool tb, hipStream_t s) {
-  static const bool timing = std::getenv("CAPGEN_HOST_TIMING") != nullptr;
-  if (!timing) return gemm_grouped_impl(ps, n, out, ta, tb, s);
+  if (!knob(Knob::HostTiming)) return gemm_grouped_impl(ps, n, out, ta, tb, s);
   static double tot = 0;
   static long cnt = 0;
   const auto t0 = std::chrono::steady_clock::now();
@@ -675,25 +631,16 @@ int gemm_tune_load(const char* path) {
   char line[1024];
   while (std::fgets(line, sizeof line, f)) {
     if (line[0] == 'g') {
-      TuneKey k{};
-      Choice c{};
-      if (std::sscanf(line + 1, "%d %d %d %d %d %d %d %d", &k.M, &k.N, &k.K, &k.ta, &k.tb, &k.out, &c.variant,
-                      &c.splitk) == 8 &&
-          c.variant >= 1 && c.variant <= NVARIANTS && c.splitk >= 1 && c.splitk <= 16) {
-        g_tuned.emplace(k, c);
+      TuneLineG t;
+      if (parse_tune_g(line + 1, NVARIANTS, &t)) {
+        g_tuned.emplace(TuneKey{t.M, t.N, t.K, t.ta, t.tb, t.out}, Choice{t.variant, t.splitk});
         ++n;
       }
     } else if (line[0] == 'G') {
-      std::vector<int> v;
-      const char* p = line + 1;
-      int x, used = 0;
-      while (std::sscanf(p, "%d%n", &x, &used) == 1) v.push_back(x), p += used;
-      const bool grouped_variant =
-          v.size() >= 5 && std::find(std::begin(kGroupVariants), std::end(kGroupVariants), v.back()) != std::end(kGroupVariants);
-      if (grouped_variant && v[3] >= 1 && v[3] <= kMaxGroup && v.size() == 4 + 3 * (size_t)v[3] + 1) {
-        const int var = v.back();  // (a stale or corrupt variant is skipped: the group is tuned again)
-        std::vector<int> key{v[0], v[1], v[2]};
-        key.insert(key.end(), v.begin() + 4, v.end() - 1);
+      std::vector<int> key;
+      int var = 0;
+      if (parse_tune_G(line + 1, kGroupVariants, (int)(sizeof kGroupVariants / sizeof kGroupVariants[0]), kMaxGroup,
+                       &key, &var)) {
         g_group_tuned.emplace(key, var);
         ++n;
       }
@@ -732,7 +679,10 @@ int gemm_tune_save(const char* path) {
 int gemm_tune_live_count() { return g_live_tuned; }
 
 void gemm_set_variant(int v) { g_variant = v; }
-void gemm_set_splitk_protocol(int p) { g_splitk_proto = p; }
+void gemm_set_splitk_protocol(int p) {
+  require(p == 0 || debug_build(), "split-K protocol bits are a debug-build diagnostic (libcapgen_debug.so)");
+  g_splitk_proto = p;
+}
 void gemm_set_timing_buf(uint64_t* p) { g_timing_buf = p; }
 void gemm_splitk_diag(int* out4, bool reset) {
   CAPGEN_HIP(hipDeviceSynchronize());
@@ -761,12 +711,13 @@ static void load_default_tune_table() {
       path = (slash == std::string::npos ? std::string(".") : path.substr(0, slash)) + "/tune_gfx950.txt";
     }
     const int n = gemm_tune_load(path.c_str());
-    if (std::getenv("CAPGEN_AUTOTUNE_LOG")) std::fprintf(stderr, "[capgen gemm] tune table %s: %d entries\n", path.c_str(), n);
+    if (knob(Knob::AutotuneLog)) std::fprintf(stderr, "[capgen gemm] tune table %s: %d entries\n", path.c_str(), n);
   });
 }
 
 void gemm_init() {
   load_default_tune_table();
+  g_splitk_proto = knob(Knob::SplitkProto);
   int dev = 0;
   CAPGEN_HIP(hipGetDevice(&dev));
   require(dev >= 0 && dev < 64, "gemm_init: device index out of range");

@@ -88,8 +88,8 @@ const char* kname(int k) { return k == WR ? "write" : k == ACC ? "accumulate" : 
 }  // namespace
 
 bool g_log = env_on("CAPGEN_HAZARD");
-int64_t g_delay = [] {
-  const char* e = std::getenv("CAPGEN_SIDE_DELAY");  // microseconds
+int64_t g_delay = [] {  // (debug build: CAPGEN_SIDE_DELAY microseconds; set_side_delay in any build)
+  const char* e = debug_build() ? std::getenv("CAPGEN_SIDE_DELAY") : nullptr;
   return e ? (int64_t)(std::atof(e) * 100.0) : (int64_t)0;
 }();
 

@@ -3,7 +3,7 @@
 
 #include <cstring>
 
-#include "capgen_common.h"
+#include "capgen_host.h"
 
 namespace capgen {
 

@@ -99,6 +99,8 @@ void adam_update(float* p, const float* g, float* m, float* v, size_t n, float b
                  const float* scal, bf16* shadow, size_t n_shadow, hipStream_t s, int grid_cap = 0,
                  const AdamTiles& tiles = AdamTiles{});
 void to_bf16(const float* src, bf16* dst, size_t n, hipStream_t s);
+// exact, order-independent checksum of an f32 arena (sum of bit patterns x (2 i + 1) mod 2^64); synchronous
+uint64_t arena_checksum(const float* p, size_t n, hipStream_t s);
 // greedy: out token = argmax(softmax(logits[b])) (first index on ties)   (model.py:126-128)
 void argmax_softmax(const float* logits, int B, int V, int64_t* ids_out, int64_t ids_ld, int col,
                     int32_t* next_ids, int64_t next_ld, hipStream_t s, int logsm = 0);

@@ -13,13 +13,6 @@
 
 namespace capgen {
 
-int skip_mask() {
-  static const int m = [] {
-    const char* e = std::getenv("CAPGEN_SKIP");
-    return e ? std::atoi(e) : 0;
-  }();
-  return m;
-}
 
 constexpr int LN_THREADS = 256;  // 4 rows per workgroup
 constexpr float LN_EPS = 1e-6f;  // modules.py:57,105
@@ -725,10 +718,8 @@ void ce_finish(const float2* stats, int64_t ld, const float* tlogit, const int32
                         rd(tgt, (int64_t)M * 4), wr(loss_row, (int64_t)M * 4), wr(dl, (int64_t)M * V * 2)});
   }
   const int spt = ((V + 15) / 16 + 255) / 256;
-  // 16-B accesses when every row starts 16-B aligned (CAPGEN_CE_VEC8=0: the 8-B form -- A/B and
-  // bit-identity test knob, read per launch: one launch per step)
-  const char* ve = std::getenv("CAPGEN_CE_VEC8");
-  const bool v8 = !(ve && ve[0] == '0') && V % 8 == 0 && ((uintptr_t)dl & 15) == 0;
+  // 16-B accesses when every row starts 16-B aligned (Knob::CeVec8 = 0: the 8-B form, bit-identity test)
+  const bool v8 = knob(Knob::CeVec8) != 0 && V % 8 == 0 && ((uintptr_t)dl & 15) == 0;
   auto go = [&](auto spt_c) {
     constexpr int S = decltype(spt_c)::value;
     if (v8) ce_finish_kernel<S, 8><<<M, 256, 0, s>>>(stats, ld, tlogit, tgt, V, pad, loss_row, dl);
@@ -794,35 +785,65 @@ void adam_prepare(int64_t* step, float lr, float b1, float b2, float* scal, hipS
 }
 
 
-__global__ void __launch_bounds__(256) adam_kernel(float4* __restrict__ p, const float4* __restrict__ g,
-                                                   float4* __restrict__ m, float4* __restrict__ v, size_t n4,
+// Adam streams 30 B per parameter that nothing else in the step reads (f32 params, grads, moments:
+// 16 B in, 12 B out) beside the critical chain, so (a) those streams use non-temporal loads and
+// stores -- they should not push the chain's GEMM panels out of the L2 / Infinity Cache -- while the
+// bf16 shadow and the tiled copies, which the next forward reads, keep the default policy; and (b)
+// every thread keeps ADAM_U 16-B loads of each array in flight (4 x ADAM_U loads issued before the
+// first use), so one workgroup per CU moves the stream at a useful rate (one load per array per
+// iteration measured 3.1 TB/s, round 4).
+constexpr int ADAM_U = 4;
+typedef float adam_f4 __attribute__((ext_vector_type(4)));  // (the nontemporal builtins take clang vectors)
+__global__ void __launch_bounds__(256) adam_kernel(adam_f4* __restrict__ p, const adam_f4* __restrict__ g,
+                                                   adam_f4* __restrict__ m, adam_f4* __restrict__ v, size_t n4,
                                                    float b1, float b2, float eps, const float* __restrict__ scal,
                                                    bf16* __restrict__ shadow, size_t n_shadow, AdamTiles tiles) {
   const float neg_step = scal[0], bc2s = scal[1];
   const float b1c = 1.f - b1, b2c = 1.f - b2;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
-    float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
-    adam_one(pp.x, gg.x, mm.x, vv.x, b1c, b2, b2c, eps, neg_step, bc2s);
-    adam_one(pp.y, gg.y, mm.y, vv.y, b1c, b2, b2c, eps, neg_step, bc2s);
-    adam_one(pp.z, gg.z, mm.z, vv.z, b1c, b2, b2c, eps, neg_step, bc2s);
-    adam_one(pp.w, gg.w, mm.w, vv.w, b1c, b2, b2c, eps, neg_step, bc2s);
-    p[i] = pp;
-    m[i] = mm;
-    v[i] = vv;
-    if (shadow && 4 * i < n_shadow) {
-      typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-      bf16x4 o = {(bf16)pp.x, (bf16)pp.y, (bf16)pp.z, (bf16)pp.w};
-      *reinterpret_cast<bf16x4*>(shadow + 4 * i) = o;
-      // the fused attention fronts' tiled copy (qkv_tile_weights layout): 4 consecutive k of one
-      // row land in one 8-B piece of the row's 16-B fragment slot
+  const size_t stride = (size_t)gridDim.x * 256 * ADAM_U;
+  for (size_t base = blockIdx.x * (size_t)(256 * ADAM_U) + threadIdx.x; base < n4; base += stride) {
+    adam_f4 pp[ADAM_U], gg[ADAM_U], mm[ADAM_U], vv[ADAM_U];
 #pragma unroll
-      for (int t = 0; t < AdamTiles::kMax; ++t) {
-        const int64_t rel = (int64_t)(4 * i) - tiles.off[t];
-        if (t < tiles.n && rel >= 0 && rel < tiles.len[t]) {
-          const int64_t row = rel >> 9;
-          const int k = (int)(rel & 511);
-          const int64_t piece = (((row >> 4) * 16 + (k >> 5)) * 64 + (row & 15) + 16 * ((k >> 3) & 3)) * 8 + (k & 7);
-          *reinterpret_cast<bf16x4*>(tiles.dst[t] + piece) = o;
+    for (int u = 0; u < ADAM_U; ++u) {
+      // (a lane past the end re-reads element base: in range, its results are not stored)
+      const size_t i = base + (size_t)u * 256 < n4 ? base + (size_t)u * 256 : base;
+      pp[u] = __builtin_nontemporal_load(p + i);
+      gg[u] = __builtin_nontemporal_load(g + i);
+      mm[u] = __builtin_nontemporal_load(m + i);
+      vv[u] = __builtin_nontemporal_load(v + i);
+    }
+    // every load above is issued before the first value is consumed (hipcc otherwise sinks each
+    // group of loads to its use, leaving one array's load in flight at a time)
+#pragma unroll
+    for (int u = 0; u < ADAM_U; ++u) asm volatile("" : "+v"(pp[u]), "+v"(gg[u]), "+v"(mm[u]), "+v"(vv[u]));
+#pragma unroll
+    for (int u = 0; u < ADAM_U; ++u) {
+      const size_t i = base + (size_t)u * 256;
+      if (i >= n4) break;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float pc = pp[u][c], mc = mm[u][c], vc = vv[u][c];
+        adam_one(pc, gg[u][c], mc, vc, b1c, b2, b2c, eps, neg_step, bc2s);
+        pp[u][c] = pc, mm[u][c] = mc, vv[u][c] = vc;
+      }
+      __builtin_nontemporal_store(pp[u], p + i);
+      __builtin_nontemporal_store(mm[u], m + i);
+      __builtin_nontemporal_store(vv[u], v + i);
+      if (shadow && 4 * i < n_shadow) {
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        bf16x4 o = {(bf16)pp[u][0], (bf16)pp[u][1], (bf16)pp[u][2], (bf16)pp[u][3]};
+        *reinterpret_cast<bf16x4*>(shadow + 4 * i) = o;
+        // the fused attention fronts' tiled copy (qkv_tile_weights layout): 4 consecutive k of one
+        // row land in one 8-B piece of the row's 16-B fragment slot
+#pragma unroll
+        for (int t = 0; t < AdamTiles::kMax; ++t) {
+          const int64_t rel = (int64_t)(4 * i) - tiles.off[t];
+          if (t < tiles.n && rel >= 0 && rel < tiles.len[t]) {
+            const int64_t row = rel >> 9;
+            const int k = (int)(rel & 511);
+            const int64_t piece = (((row >> 4) * 16 + (k >> 5)) * 64 + (row & 15) + 16 * ((k >> 3) & 3)) * 8 + (k & 7);
+            *reinterpret_cast<bf16x4*>(tiles.dst[t] + piece) = o;
+          }
         }
       }
     }
@@ -833,7 +854,9 @@ void adam_update(float* p, const float* g, float* m, float* v, size_t n, float b
                  const AdamTiles& tiles) {
   require(tiles.n >= 0 && tiles.n <= AdamTiles::kMax, "adam: at most kMax tiled ranges");
   for (int t = 0; t < tiles.n; ++t)
-    require(shadow && tiles.off[t] % 512 == 0 && tiles.len[t] % (16 * 512) == 0 && tiles.off[t] >= 0 &&
+    // (the tile formula needs only the element offset from the matrix start; 4-aligned so a thread's
+    // 4 elements stay in one row)
+    require(shadow && tiles.off[t] % 4 == 0 && tiles.len[t] % (16 * 512) == 0 && tiles.off[t] >= 0 &&
                 tiles.off[t] + tiles.len[t] <= (int64_t)n_shadow && tiles.dst[t],
             "adam: a tiled range must be whole 16-row blocks of 512-wide rows inside the shadow range");
   require(n % 4 == 0 && n_shadow % 4 == 0, "adam: arena size must be a multiple of 4");
@@ -846,16 +869,36 @@ void adam_update(float* p, const float* g, float* m, float* v, size_t n, float b
                        hz::wr(tiles.n > 2 ? tiles.dst[2] : nullptr, tiles.n > 2 ? tiles.len[2] * 2 : 0),
                        hz::wr(tiles.n > 3 ? tiles.dst[3] : nullptr, tiles.n > 3 ? tiles.len[3] * 2 : 0)});
   size_t n4 = n / 4;
-  static const int cap = [] {  // Adam workgroups (grid-stride): one per CU leaves the other wave slots to the
-    // critical stream (A/B over 4 runs each: 3.046 vs 3.070 ms/step with 8 per CU; CAPGEN_ADAM_GRID)
-    const char* e = std::getenv("CAPGEN_ADAM_GRID");
-    return e ? std::max(1, std::atoi(e)) : 256;
-  }();
+  // Adam workgroups (grid-stride): one per CU leaves the other wave slots to the critical stream
+  // (A/B over 4 runs each: 3.046 vs 3.070 ms/step with 8 per CU)
+  constexpr int cap = 256;
   // grid_cap > 0: the caller's cap (an update on the step's critical path takes the whole chip)
-  int grid = (int)std::min<size_t>((n4 + 255) / 256, (size_t)(grid_cap > 0 ? grid_cap : cap));
-  adam_kernel<<<grid, 256, 0, s>>>((float4*)p, (const float4*)g, (float4*)m, (float4*)v, n4, b1, b2, eps, scal,
+  int grid = (int)std::min<size_t>((n4 + 256 * ADAM_U - 1) / (256 * ADAM_U), (size_t)(grid_cap > 0 ? grid_cap : cap));
+  adam_kernel<<<grid, 256, 0, s>>>((adam_f4*)p, (const adam_f4*)g, (adam_f4*)m, (adam_f4*)v, n4, b1, b2, eps, scal,
                                    shadow, n_shadow, tiles);
   CAPGEN_HIP(hipGetLastError());
+}
+
+// Position-weighted sum of the f32 bit patterns, sum_i bits(x_i) * (2 i + 1) mod 2^64: exact and
+// independent of summation order, so equal arenas give equal values on every rank / run.
+__global__ void checksum_kernel(const uint32_t* __restrict__ x, size_t n, unsigned long long* out) {
+  unsigned long long acc = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    acc += (unsigned long long)x[i] * (2ull * i + 1ull);
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, acc);
+}
+uint64_t arena_checksum(const float* p, size_t n, hipStream_t s) {
+  unsigned long long* d = nullptr;
+  CAPGEN_HIP(hipMalloc(&d, sizeof *d));
+  CAPGEN_HIP(hipMemsetAsync(d, 0, sizeof *d, s));
+  checksum_kernel<<<1024, 256, 0, s>>>(reinterpret_cast<const uint32_t*>(p), n, d);
+  CAPGEN_HIP(hipGetLastError());
+  unsigned long long v = 0;
+  CAPGEN_HIP(hipMemcpyAsync(&v, d, sizeof v, hipMemcpyDeviceToHost, s));
+  CAPGEN_HIP(hipStreamSynchronize(s));
+  CAPGEN_HIP(hipFree(d));
+  return v;
 }
 
 __global__ void to_bf16_kernel(const float* __restrict__ src, bf16* __restrict__ dst, size_t n) {

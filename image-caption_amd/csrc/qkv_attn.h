@@ -19,7 +19,6 @@ struct QkvAttn {
   // cross attention (DecoderBlock's second MHA, modules.py:195-197): only q = X . Wq^T is projected
   // (W = Wq [d][d], qkv = the q buffer); K / V come from g.k / g.v (the precomputed cross K/V)
   int cross = 0;
-  int clamp = 0;  // rows past L / Lk: 0 = not loaded (default), 1 = loaded from the last row (A/B)
 };
 bool qkv_attn_ok(const QkvAttn& a);
 // The fronts read their projection weights TILED: the 64 lanes' 16-B MFMA fragments of 16-row block j
@@ -43,7 +42,6 @@ struct QkvBwd {
   bf16* dq = nullptr;
   bf16* dk = nullptr;
   bf16* dv = nullptr;
-  int clamp = 0;  // as QkvAttn::clamp
 };
 bool qkv_bwd_ok(const QkvBwd& a);
 void qkv_attn_bwd(const QkvBwd& a, hipStream_t s);

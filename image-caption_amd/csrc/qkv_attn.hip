@@ -66,7 +66,8 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
   const int L = g.Lq;     // rows of X (query rows)
   const bf16* xb = a.X + (int64_t)b * L * a.ldx;
 
-  // ---- first weight batch, X rows (clamped row, unconditional: no load waits at a branch join),
+  // ---- first weight batch, X rows (rows past L not loaded: in the step that beat re-reading the last
+  // row, round 4),
   // key flags; then the LDS writes: X (rows >= L zero), zeroed attention images.
   // Projection: wave w -> columns 48w .. 48w+47 of [q_h | k_h | v_h]. ----
   const int fr = lane & 15, fg = lane >> 4;
@@ -89,10 +90,10 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int c = tid + 256 * u, row = c / (QD / 8), ch = c % (QD / 8);
-      v[u] = row < L || a.clamp ? *reinterpret_cast<const uint4*>(xb + (int64_t)min(row, L - 1) * a.ldx + ch * 8)
+      v[u] = row < L ? *reinterpret_cast<const uint4*>(xb + (int64_t)min(row, L - 1) * a.ldx + ch * 8)
                                 : uint4{0u, 0u, 0u, 0u};
     }
-    // cross attention: K / V head slices from memory (rows < Lk, clamped, unconditional)
+    // cross attention: K / V head slices from memory (rows < Lk)
     uint4 kv[2][2];
     if constexpr (NP == 1) {
       const int bk = g.kv_bmod ? b % g.kv_bmod : b;
@@ -104,7 +105,7 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const int c = tid + 256 * u, row = c >> 3, ch = c & 7;
-          kv[i][u] = row < g.Lk || a.clamp
+          kv[i][u] = row < g.Lk
                          ? *reinterpret_cast<const uint4*>(src[i] + (int64_t)min(row, g.Lk - 1) * ld[i] + ch * 8)
                          : uint4{0u, 0u, 0u, 0u};
         }
@@ -232,7 +233,7 @@ __global__ void __launch_bounds__(256) qkv_attn_bwd_kernel(QkvBwd a) {
 #pragma unroll
   for (int u = 0; u < PER; ++u) {
     const int c = tid + 256 * u, row = c / (QD / 8), ch = c % (QD / 8);
-    xv[u] = row < L || a.clamp ? *reinterpret_cast<const uint4*>(xb + (int64_t)min(row, L - 1) * a.ldda + ch * 8)
+    xv[u] = row < L ? *reinterpret_cast<const uint4*>(xb + (int64_t)min(row, L - 1) * a.ldda + ch * 8)
                                : uint4{0u, 0u, 0u, 0u};
   }
   const int bk = g.kv_bmod ? b % g.kv_bmod : b;
@@ -247,7 +248,7 @@ __global__ void __launch_bounds__(256) qkv_attn_bwd_kernel(QkvBwd a) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int c = tid + 256 * u, row = c >> 3, ch = c & 7;
-      kqv[i][u] = row < Ls[i] || a.clamp
+      kqv[i][u] = row < Ls[i]
                       ? *reinterpret_cast<const uint4*>(src[i] + (int64_t)min(row, Ls[i] - 1) * ld[i] + ch * 8)
                       : uint4{0u, 0u, 0u, 0u};
     }
@@ -344,18 +345,8 @@ bool qkv_attn_ok(const QkvAttn& a) {
          a.ldx % 8 == 0 && a.ldqkv % 8 == 0 && g.o_ld % 8 == 0 && g.o_bs % 8 == 0;
 }
 
-// CAPGEN_QKV_CLAMP=1 (A/B knob): load the staged rows past L / Lk from the last row instead of skipping them
-static int qkv_clamp() {
-  static const int c = [] {
-    const char* e = std::getenv("CAPGEN_QKV_CLAMP");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  return c;
-}
-
 void qkv_attn_fwd(const QkvAttn& a_in, hipStream_t s) {
   QkvAttn a = a_in;
-  a.clamp = qkv_clamp();
   require(qkv_attn_ok(a), "qkv_attn_fwd: unsupported geometry (head size 64, d = 512, self attention, L <= 64)");
   const AttnGeom& g = a.g;
   if (hz::active()) {
@@ -393,14 +384,15 @@ void qkv_attn_fwd(const QkvAttn& a_in, hipStream_t s) {
 
 bool qkv_bwd_ok(const QkvBwd& a) {
   const AttnGeom& g = a.g;
-  return g.dk == DK && g.H * DK == QD && g.Lq >= 1 && g.Lq <= 64 && g.Lk >= 1 && g.Lk <= 64 && !g.kv_row && a.Wt &&
+  // (kv_bmod: K / V shared by several images -- decode only; the staged backward writes dk / dv per image)
+  return g.dk == DK && g.H * DK == QD && g.Lq >= 1 && g.Lq <= 64 && g.Lk >= 1 && g.Lk <= 64 && !g.kv_row &&
+         g.kv_bmod == 0 && a.Wt &&
          a.dA && a.dq && a.dk && a.dv && a.ldda % 8 == 0 && g.q_ld % 8 == 0 && g.k_ld % 8 == 0 && g.v_ld % 8 == 0 &&
          g.q_bs % 8 == 0 && g.k_bs % 8 == 0 && g.v_bs % 8 == 0;
 }
 
 void qkv_attn_bwd(const QkvBwd& a_in, hipStream_t s) {
   QkvBwd a = a_in;
-  a.clamp = qkv_clamp();
   require(qkv_bwd_ok(a), "qkv_attn_bwd: unsupported geometry (head size 64, d = 512, Lq / Lk <= 64)");
   const AttnGeom& g = a.g;
   if (hz::active()) {

@@ -13,7 +13,7 @@
 #include <cstdint>
 #include <vector>
 
-#include "capgen_common.h"
+#include "capgen_host.h"
 
 namespace capgen {
 namespace {

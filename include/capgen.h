@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define CAPGEN_ABI_VERSION 8
+#define CAPGEN_ABI_VERSION 9
 
 typedef struct capgen_engine capgen_t;
 
@@ -73,6 +73,13 @@ typedef struct capgen_param_info {
 
 const char* capgen_last_error(void);
 int capgen_abi_version(void);
+/* Run-time switches (csrc/knobs.cpp): name without the CAPGEN_ prefix (e.g. "FUSED_CE").  The
+ * CAPGEN_<NAME> environment sets the process default when the library first asks; this call changes
+ * it afterwards (engines read theirs when created).  Non-zero status for an unknown name or a
+ * debug-build-only switch in the product library.  *old (may be null) receives the previous value.
+ * capgen_debug_build: 1 in libcapgen_debug.so (-DCAPGEN_DEBUG), else 0. */
+int capgen_set_knob(const char* name, int value, int* old);
+int capgen_debug_build(void);
 
 /* Host-only (no device needed): the parameter table for a config.  Writes up to `cap`
  * entries, sets *count to the total; *arena_elems = arena size in f32 elements. */
@@ -284,6 +291,13 @@ int capgen_dp_set_global_count(capgen_t* h, float count);
  * capgen_dp_debug_shard (test hook): without any collective, update as rank `rank` of `world`
  * would (Adam on this rank's chunks only); world <= 1 turns it off. */
 int capgen_dp_sync_adam_state(capgen_t* h);
+/* The engine communicator's size and this rank (ncclCommCount / ncclCommUserRank; 0 / 0 before
+ * capgen_dp_init).  At world > 1 the FIRST capgen_train_step also checks, once, that every rank holds
+ * the same global non-pad count and loss (max == min over the ranks) and fails the step otherwise. */
+int capgen_dp_comm_info(capgen_t* h, int* nranks, int* rank);
+/* Exact, order-independent checksum of the f32 parameter arena (sum of the bit patterns times
+ * (2 i + 1), mod 2^64; synchronous): equal parameters give equal values on every rank. */
+int capgen_params_checksum(capgen_t* h, uint64_t* out);
 int capgen_dp_buckets(capgen_t* h, int64_t* offs, int64_t* counts, int cap, int* n);
 int capgen_dp_debug_shard(capgen_t* h, int rank, int world);
 

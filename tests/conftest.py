@@ -19,3 +19,19 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
+
+
+@pytest.fixture
+def set_knob():
+    """set_knob(name, value): a library run-time switch (capgen_set_knob, name without CAPGEN_) for the
+    test; every switch it touched is restored afterwards."""
+    from capgen import _lib
+    saved = {}
+
+    def _set(name, value):
+        old = _lib.set_knob(name, int(value))
+        saved.setdefault(name, old)
+
+    yield _set
+    for name, old in saved.items():
+        _lib.set_knob(name, old)

@@ -162,19 +162,19 @@ def test_dp_world1_rccl_train_step_fp32(graph):
 
 
 @pytest.mark.parametrize("dp", [False, True])
-def test_split_forward_graphs_equal_eager_fp32(monkeypatch, dp):
+def test_split_forward_graphs_equal_eager_fp32(set_knob, dp):
     """The forward as split linear graphs (pre / decoder front on es2 / encoder / decoder, events
     between them; CAPGEN_FWD_SPLIT=1) equals the eager
     forward over three bucketed train steps, with and without the RCCL DP path (world 1)."""
     from capgen.engine import Engine
     cfg, seed, z = load_fixture("c2s")
     f, p, c = _inputs(z)
-    monkeypatch.setenv("CAPGEN_FWD_SPLIT", "1")
+    set_knob("FWD_SPLIT", 1)
     a = _engine(cfg, seed)
-    monkeypatch.setenv("CAPGEN_FWD_GRAPH", "0")
+    set_knob("FWD_GRAPH", 0)
     b = _engine(cfg, seed)
-    monkeypatch.delenv("CAPGEN_FWD_SPLIT")
-    monkeypatch.delenv("CAPGEN_FWD_GRAPH")
+    set_knob("FWD_SPLIT", 0)
+    set_knob("FWD_GRAPH", 1)
     for e in (a, b):
         e.set_training(False)
         if dp:
@@ -352,16 +352,16 @@ def test_c3_eight_ranks_of_64_equal_global_batch_512_fp32():
 
 
 @pytest.mark.parametrize("graph", [False, True])
-def test_sharded_update_world1_rccl_fp32(monkeypatch, graph):
+def test_sharded_update_world1_rccl_fp32(set_knob, graph):
     """The sharded update's RCCL calls (in-place reduce-scatter of each bucket, Adam on the
     chunk, in-place all-gather, local bf16 re-cast) at world size 1 (CAPGEN_ZERO=2 forces the
     path) equal the single-process step."""
     from capgen.engine import Engine
-    monkeypatch.setenv("CAPGEN_ZERO", "2")
+    set_knob("ZERO", 2)
     cfg, seed, z = load_fixture("c1")
     f, p, c = _inputs(z)
     a = _engine(cfg, seed)
-    monkeypatch.delenv("CAPGEN_ZERO")
+    set_knob("ZERO", 1)
     b = _engine(cfg, seed)
     for e in (a, b):
         e.set_training(False)
@@ -486,7 +486,7 @@ def test_bf16_mode_loss_close(tag):
 
 
 @pytest.mark.parametrize("tag", ["c2s", "c1_focal", "padcap"])
-def test_fused_classifier_ce_equals_logits_path_bf16(tag, monkeypatch):
+def test_fused_classifier_ce_equals_logits_path_bf16(tag, set_knob):
     """The bf16 step's fused classifier + CE (GEMM epilogue: exp(v - slab max) + per-16-column
     slab stats, never the logits; ce_finish: lse, loss rows, softmax - onehot in place;
     model.py:93-96) vs the f32-logits path (CAPGEN_FUSED_CE=0) on the same weights: loss within
@@ -502,7 +502,7 @@ def test_fused_classifier_ce_equals_logits_path_bf16(tag, monkeypatch):
         f, p, c = _inputs(z)
     out = []
     for dt, fused in (("bf16", "1"), ("bf16", "0"), ("fp32", "1")):
-        monkeypatch.setenv("CAPGEN_FUSED_CE", fused)
+        set_knob("FUSED_CE", fused)
         e = _engine(cfg, seed, dtype=dt)
         e.set_training(False)
         loss = e.forward(f, p, c).item()
@@ -548,16 +548,16 @@ def test_bf16_train_mode_matches_fp32_with_dropout():
         assert rel < 0.2, (n, rel)
 
 
-def test_grouped_weight_gradients_match_single_launches_bf16(monkeypatch):
+def test_grouped_weight_gradients_match_single_launches_bf16(set_knob):
     """bf16 weight gradients of one block computed by ONE grouped launch (default) equal the
     per-weight launches (CAPGEN_GROUP_DW=0) up to f32 summation order (split-K choices), with the
     default streams (round 3 ran it on one stream while the >= 2-stream divergence was open;
     DESIGN.md section 6)."""
     cfg, seed, z = load_fixture("c2s")
     f, p, c = _inputs(z)
-    monkeypatch.setenv("CAPGEN_GROUP_DW", "0")
+    set_knob("GROUP_DW", 0)
     a = _engine(cfg, seed, dtype="bf16", dropout=0.3)
-    monkeypatch.delenv("CAPGEN_GROUP_DW")
+    set_knob("GROUP_DW", 1)
     b = _engine(cfg, seed, dtype="bf16", dropout=0.3)
     for e in (a, b):
         e.set_training(True)
@@ -625,9 +625,9 @@ def test_train_step_equals_forward_backward_adam_bf16(graph, monkeypatch):
             assert frac < 0.01, (k, frac)
 
 
-def _bit_reproducible_run(monkeypatch, streams):
+def _bit_reproducible_run(set_knob, streams):
     if streams:
-        monkeypatch.setenv("CAPGEN_STREAMS", str(streams))
+        set_knob("STREAMS", streams)
     cfg, seed, z = load_fixture("c2s")
     f, p, c = _inputs(z)
     for _ in range(4):
@@ -645,7 +645,7 @@ def _bit_reproducible_run(monkeypatch, streams):
         assert not bad, bad
 
 
-def test_bf16_weight_gradients_bit_reproducible(monkeypatch):
+def test_bf16_weight_gradients_bit_reproducible(set_knob):
     """Two engines with the same weights and batch produce bit-identical Linear weight gradients
     in bf16 mode, four times over (every GEMM, the split-K combine and the grouped launches are
     deterministic; only LayerNorm/bias sums use f32 atomics).  c2s has 2 x 36 = 72 encoder
@@ -653,14 +653,14 @@ def test_bf16_weight_gradients_bit_reproducible(monkeypatch):
     once read past the activation (gemm_bf16.hip Op::issue; 9 of 16 runs diverged).  One stream
     per engine: the kernels' own determinism (each kernel class is also bit-stable beside a
     co-scheduled noise stream, tools/cosched_probe.py)."""
-    _bit_reproducible_run(monkeypatch, 1)
+    _bit_reproducible_run(set_knob, 1)
 
 
-def test_bf16_weight_gradients_bit_reproducible_multistream(monkeypatch):
+def test_bf16_weight_gradients_bit_reproducible_multistream(set_knob):
     """The same with the default three streams (weight gradients on the side stream).  Was the
     open divergence of round 3 until the LayerNorm backward went to one row per wave
     (DESIGN.md section 6)."""
-    _bit_reproducible_run(monkeypatch, 0)
+    _bit_reproducible_run(set_knob, 0)
 
 
 def test_dropout_backward_directional_derivative_fp32():
@@ -937,7 +937,7 @@ def test_attention_kernels_vs_torch(dtype, B, H, Lq, Lk, dk, causal, mask):
 
 @pytest.mark.parametrize("B,Lq,Lk,causal,mask", [(5, 5, 36, 0, True), (4, 16, 36, 0, True), (3, 12, 19, 1, True),
                                                   (2, 3, 64, 0, False), (256, 5, 36, 0, False)])
-def test_attention_one_wave_kernel_bit_identical(monkeypatch, B, Lq, Lk, causal, mask):
+def test_attention_one_wave_kernel_bit_identical(set_knob, B, Lq, Lk, causal, mask):
     """The one-wave bf16 attention forward for Lq <= 16 (attention_mfma.hip attn_fwd_wave_kernel: the
     beam's cross attention at decode) returns the same bits as the 4-wave kernel's wave 0
     (CAPGEN_ATTN_WAVE=0), probabilities included."""
@@ -955,7 +955,7 @@ def test_attention_one_wave_kernel_bit_identical(monkeypatch, B, Lq, Lk, causal,
     ptr = lambda t: C.c_void_p(t.data_ptr())
     out = []
     for wave in ("1", "0"):
-        monkeypatch.setenv("CAPGEN_ATTN_WAVE", wave)
+        set_knob("ATTN_WAVE", wave)
         o = torch.full_like(q, float("nan"))
         probs = torch.full((B, H, Lq, Lk), float("nan"), device=DEV)
         _lib.check(lib.capgen_debug_attention(1, B, H, Lq, Lk, 64, ptr(q), ptr(k), ptr(v), ptr(vd) if mask else None,
@@ -1395,17 +1395,17 @@ def test_train_loop_end_to_end_on_device(tmp_path):
 
 
 @pytest.mark.parametrize("tag", ["c1", "c2s", "c1_imgobj", "c1_movefirst"])
-def test_decode_graph_replay_matches_eager(tag, monkeypatch):
+def test_decode_graph_replay_matches_eager(tag, set_knob):
     """Greedy and beam decoding replayed as captured hipGraphs (1st call eager, 2nd captures,
     later ones replay) equal the eager engine bit for bit, match the reference fixtures, and
     read the CURRENT weights after an Adam step in between."""
     cfg, seed, z = load_fixture(tag)
     f, p, c = _inputs(z)
-    monkeypatch.setenv("CAPGEN_GEN_GRAPH", "1")
+    set_knob("GEN_GRAPH", 1)
     a = _engine(cfg, seed)
-    monkeypatch.setenv("CAPGEN_GEN_GRAPH", "0")
+    set_knob("GEN_GRAPH", 0)
     b = _engine(cfg, seed)
-    monkeypatch.delenv("CAPGEN_GEN_GRAPH")
+    set_knob("GEN_GRAPH", 0)
     for e in (a, b):
         e.set_training(False)
         e.forward(f, p, c)  # size the training workspace first: no reallocation inside the loop
@@ -1632,7 +1632,7 @@ def test_c4_bf16_decode_matches_fp32_within_margin():
           f"beam {nb}/256 differ, worst score deficit {worst:.3g} <= {tol:.3g}")
 
 
-def test_slab_decode_selection_equals_full_row(monkeypatch):
+def test_slab_decode_selection_equals_full_row(set_knob):
     """bf16 decode: the classifier epilogue's slab stats + k-best-slab selection (ops.hip
     slab_argmax / slab_row_topk_kernel) against the full-row kernels (CAPGEN_SLAB_DECODE=0) at C4
     (B=256, V=10000, beam 5).  Both read the same f32 logits (the epilogue stores v exactly as the
@@ -1642,7 +1642,7 @@ def test_slab_decode_selection_equals_full_row(monkeypatch):
     differing image's sequence score (fp32 engine, sum of probabilities, model.py:183) within 1e-5."""
     _, cfg, sd, e32, f, p, c = _c2_setup(B=256, dtype="fp32", weights="fixture")
     _, _, _, slab, _, _, _ = _c2_setup(B=256, dtype="bf16", weights="fixture")
-    monkeypatch.setenv("CAPGEN_SLAB_DECODE", "0")
+    set_knob("SLAB_DECODE", 0)
     _, _, _, full, _, _, _ = _c2_setup(B=256, dtype="bf16", weights="fixture")
     for e in (slab, full, e32):
         e.set_training(False)
@@ -1669,30 +1669,30 @@ def test_slab_decode_selection_equals_full_row(monkeypatch):
             assert (score(bs[diff]) - score(bf[diff])).abs().max().item() < 1e-5
 
 
-def test_grouped_decode_attention_lds_staging_bit_identical(monkeypatch):
+def test_grouped_decode_attention_lds_staging_bit_identical(set_knob):
     """bf16 beam decode at C4 (B=256, beam 5): the grouped cross-attention with the image's K/V
     staged in LDS once per (image, head) workgroup (CAPGEN_DECODE_GROUP_LDS, default) gives the same
     beam ids as the per-wave register loads (same per-lane values, same sums)."""
-    monkeypatch.setenv("CAPGEN_DECODE_CROSS_MFMA", "0")  # (the beam cross attention on the grouped kernel)
+    set_knob("DECODE_CROSS_MFMA", 0)  # (the beam cross attention on the grouped kernel)
     _, cfg, sd, e, f, p, c = _c2_setup(B=256, dtype="bf16", weights="fixture")
     e.set_training(False)
     fd, pd = f.to(DEV).bfloat16(), p.to(DEV)
-    monkeypatch.setenv("CAPGEN_DECODE_GROUP_LDS", "1")
+    set_knob("DECODE_GROUP_LDS", 1)
     a = e.beam(fd, pd, 5).clone()
-    monkeypatch.setenv("CAPGEN_DECODE_GROUP_LDS", "0")
+    set_knob("DECODE_GROUP_LDS", 0)
     b = e.beam(fd, pd, 5).clone()
     torch.cuda.synchronize()
     assert torch.equal(a, b)
 
 
-def test_ce_finish_16b_accesses_bit_identical(monkeypatch):
+def test_ce_finish_16b_accesses_bit_identical(set_knob):
     """ce_finish (the fused classifier + CE's second half, ops.hip) with 16-B row accesses gives the
     same loss and Linear weight gradients, bit for bit, as its 8-B form (CAPGEN_CE_VEC8=0): bf16 C2
     step.  (LayerNorm / bias sums and the word-embedding scatter use f32 atomics, whose order varies
     run to run: those to 1e-4, as in test_bf16_weight_gradients_bit_reproducible.)"""
     out = []
     for v in ("1", "0"):
-        monkeypatch.setenv("CAPGEN_CE_VEC8", v)
+        set_knob("CE_VEC8", v)
         _, cfg, sd, e, f, p, c = _c2_setup(dtype="bf16", weights="fixture")
         e.set_training(False)
         loss = e.forward(f.to(DEV).bfloat16(), p.to(DEV), c.to(DEV)).item()
@@ -1708,8 +1708,8 @@ def test_ce_finish_16b_accesses_bit_identical(monkeypatch):
             assert torch.allclose(a, b, rtol=1e-4, atol=1e-7 * a.abs().max().item()), n
 
 
-@pytest.mark.parametrize("knob", ["CAPGEN_FUSED_QKV", "CAPGEN_DECODE_CROSS_MFMA", "CAPGEN_FUSED_ATTN_BWD"])
-def test_fused_attention_fronts_track_separate_launches_bf16(monkeypatch, knob):
+@pytest.mark.parametrize("knob", ["FUSED_QKV", "DECODE_CROSS_MFMA", "FUSED_ATTN_BWD"])
+def test_fused_attention_fronts_track_separate_launches_bf16(set_knob, knob):
     """The fused self / cross attention fronts (qkv_attn.hip; CAPGEN_FUSED_QKV, default on) against the
     GEMM + attention launches they replace, and the beam decode's cross attention on the MFMA attention
     kernel (CAPGEN_DECODE_CROSS_MFMA, default on) against the grouped VALU decode kernel, on bench.py's
@@ -1720,9 +1720,9 @@ def test_fused_attention_fronts_track_separate_launches_bf16(monkeypatch, knob):
     engine's agreement with the fp32 engine's sequences is within 5 points of the separate engine's
     (beam search flips near-tied hypotheses on last-bit changes; measured 61/64 identical between the two
     bf16 engines on one run), and the two bf16 engines agree on at least 90 %."""
-    monkeypatch.setenv(knob, "0")
+    set_knob(knob, 0)
     _, cfg, sd, e0, f, p, c = _c2_setup(dtype="bf16", weights="fixture")
-    monkeypatch.delenv(knob)
+    set_knob(knob, 1)
     _, _, _, e1, _, _, _ = _c2_setup(dtype="bf16", weights="fixture")
     _, _, _, e32, _, _, _ = _c2_setup(dtype="fp32", weights="fixture")
     fd, pd, cd = f.to(DEV), p.to(DEV), c.to(DEV)

@@ -108,6 +108,52 @@ def test_dp_exact_mean_gloo_world2_matches_single_process():
     np.testing.assert_allclose(g_dp, g, atol=1e-6, rtol=1e-4)
 
 
+def _boot_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from capgen.dp import global_target_count, init_engine_dp, local_target_count, shard_seed
+
+    class RecEngine:  # stands in for Engine.dp_init (the RCCL side needs a GPU per rank)
+        def dp_init(self, uid, r, w):
+            self.args = (uid, r, w)
+
+    made = []
+
+    def unique_id():  # rank 0 only: the RCCL unique id's 128 bytes
+        made.append(rank)
+        return bytes((7 * i + 3) % 256 for i in range(128))
+
+    eng = RecEngine()
+    init_engine_dp(eng, rank, world, unique_id=unique_id)
+    _, _, caps = synthetic_batch(4 + 3 * rank, 6, 16, 84, 12, 1000, seed=shard_seed(1000, rank), min_valid=2)
+    out.put((rank, eng.args, made, local_target_count(caps), global_target_count(caps)))
+    dist.destroy_process_group()
+
+
+def test_dp_bootstrap_gloo_world2():
+    """capgen/dp.py's bootstrap over a real process group (gloo, world 2): rank 0 alone makes the
+    unique id, every rank's dp_init receives rank 0's 128 bytes with its own rank and the world size,
+    and the global non-pad count (the CE denominator, model.py:76) is the sum of the ranks' local
+    counts on both ranks, for ranks with different batch sizes and caption padding."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + os.getpid() % 1000
+    procs = [ctx.Process(target=_boot_worker, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = sorted(q.get(timeout=300) for _ in range(2))
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    uid0 = bytes((7 * i + 3) % 256 for i in range(128))
+    locals_ = [r[3] for r in res]
+    assert locals_[0] != locals_[1]
+    for rank, (uid, r, w), made, _, glob in res:
+        assert uid == uid0 and r == rank and w == 2
+        assert made == ([0] if rank == 0 else [])
+        assert glob == sum(locals_)
+
+
 def test_train_loop_cadence_matches_main_py(tmp_path):
     """capgen.train.train restates main.py:25-153: train_step per batch, compute_loss on the two
     fixed eval batches every 100 steps, a greedy sample every 2500, per-epoch valid captions +
