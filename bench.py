@@ -67,6 +67,8 @@ def dominant_class(eng, args, steps=3):
             if len(words) < 2:
                 continue
             kind = " ".join(words[1:3]) if words[1] == "gemm" and len(words) >= 3 else words[1]
+            if words[0] != "crit":  # launches off the critical stream form classes of their own
+                kind = words[0] + " " + kind
             fl = 0.0
             if words[1] == "gemm" and "x" in words[-1]:
                 m, n_, k = (int(x) for x in words[-1].split("x"))

@@ -91,8 +91,14 @@ struct Op {
   // write to the staging array and emitted `s_waitcnt vmcnt(0)` before the next ds_read of ANY
   // stage, draining every prefetch one step early (guide cdna_hip_programming.md §5 item 4(a));
   // the k-loop retires the DMA itself with counted vmcnt waits + a raw barrier (wait_younger).
+  // `s_nop 4` opens the statement: hipcc pads no hazard into or out of an asm string, and the
+  // descriptor / soffset SGPRs may come straight from a VALU write (v_readlane when hipcc restores
+  // spilled SGPRs, v_readfirstlane) -- VALU-writes-SGPR -> VMEM-reads-it needs 5 wait states, and
+  // the M0 write just before the statement 1.  Without them the DMA read a stale descriptor: the
+  // round-4 persistent FFN's wrong W2 tiles (a kernel whose SGPR pressure made hipcc restore the W2
+  // operand's descriptor by v_readlane right before the DMA; tools/persist_ffn.py).
   __device__ __forceinline__ void dma(uint32_t v, uint32_t soff, char* lds) const {
-    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(v), "s"(rsrc), "s"(soff),
+    asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(v), "s"(rsrc), "s"(soff),
                  "{m0}"((unsigned)(uintptr_t)lds)
                  : "memory");
   }

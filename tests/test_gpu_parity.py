@@ -1462,9 +1462,12 @@ def test_c2_full_size_fp32_matches_oracle():
     arithmetic (the fp32 CPU oracle) is up to 3.2e-3 of max|g| away from float64
     (decoder.5 position_wise_1.weight; 1.4e-3 even with the fixture weights), so an fp32-vs-fp32
     comparison at 1e-3 measures two fp32 rounding patterns, not parity.  Each engine tensor must be
-    within 1e-3 of max|g| of the float64 result, or within 5x the reference fp32 arithmetic's own
-    error on that tensor (measured worst: 3.1x, encoder block 0's FFN-up weight, the end of the
-    12-block f32 chain)."""
+    within 1e-3 of max|g| of the float64 result, or within 2x the reference fp32 arithmetic's own
+    error on that tensor -- 5x for the FFN-up (position_wise_1) weights and biases, whose error is set
+    by ReLU'-mask flips: a pre-activation within rounding of zero is positive in one fp32 arithmetic and
+    not in the other, which adds or drops a whole dH element from that column's sum (measured: those
+    tensors at 3.0-3.9x, every other tensor at most 1.34x the CPU's own error; round 5 summed the f32
+    GEMMs' K in 64-deep panels without moving them, gpurun_out / profiles r05_c2_grad_errors.json)."""
     O, cfg, sd, e, f, p, c = _c2_setup()
     e.set_training(False)
     loss = e.forward(f.to(DEV), p.to(DEV), c.to(DEV)).item()
@@ -1485,7 +1488,8 @@ def test_c2_full_size_fp32_matches_oracle():
         got = g[n].double().reshape(ref.shape)
         cpu32 = P[n].grad.double()
         ref_err = (cpu32 - ref).abs().max().item()  # the reference's fp32 arithmetic vs exact
-        bound = max(1e-3 * ref.abs().max().item(), 5 * ref_err) + 1e-9
+        mult = 5 if "position_wise_1" in n else 2
+        bound = max(1e-3 * ref.abs().max().item(), mult * ref_err) + 1e-9
         err = (got - ref).abs().max().item()
         report.append({"tensor": n, "max_abs_grad": ref.abs().max().item(), "engine_err": err, "ref_fp32_err": ref_err,
                        "err_over_1e-3max": err / (1e-3 * ref.abs().max().item() + 1e-30),
