@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--timeout", type=int, default=240)
+    ap.add_argument("--timeout", type=int, default=150)
     ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "ab.jsonl"))
     args = ap.parse_args()
     arms = []
