@@ -192,14 +192,25 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // ---- counter-based dropout RNG --------------------------------------------------------
-// keep(seed, site, idx): a splitmix64-style finaliser of (seed, site, idx).  Masks are
-// regenerated bit-identically in the backward pass, so nothing is stored.
+// keep(seed, site, idx): a 32-bit avalanche hash (lowbias32: 2 multiplies, 3 xor-shifts) of the
+// element index xored with a per-(step seed, site) key.  The key is the same hash of the seed and
+// site, loop-invariant in every kernel (hoisted), so a mask element costs ~9 32-bit VALU operations
+// (the splitmix64 finaliser of rounds 1-4 took ~3x that in 64-bit multiplies -- it is evaluated per
+// attention probability and per LayerNorm element, in the forward and again in the backward).
+// Masks are regenerated bit-identically in the backward pass, so nothing is stored.
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t drop_key(uint64_t seed, uint32_t site) {
+  return lowbias32((uint32_t)seed ^ lowbias32((uint32_t)(seed >> 32) + 0x9E3779B9u * (site + 1u)));
+}
 __device__ __forceinline__ uint32_t mix32(uint64_t seed, uint32_t site, uint32_t idx) {
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (((uint64_t)site << 32) | idx) + 0x632BE59BD9B4E019ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= (z >> 31);
-  return (uint32_t)(z >> 32);
+  return lowbias32(idx ^ drop_key(seed, site));
 }
 // true = keep.  p in [0,1).  threshold = p * 2^32.
 __device__ __forceinline__ bool drop_keep(uint64_t seed, uint32_t site, uint32_t idx, uint32_t thresh) {
