@@ -663,15 +663,25 @@ def test_bf16_weight_gradients_bit_reproducible_multistream(set_knob):
     _bit_reproducible_run(set_knob, 0)
 
 
-def test_dropout_backward_directional_derivative_fp32():
-    """Train-mode (dropout on) gradient vs a central finite difference of the same
-    dropout mask (RNG reset before each forward)."""
+@pytest.mark.parametrize("rng_seed", [7, 1, 4])
+def test_dropout_backward_directional_derivative_fp32(rng_seed):
+    """Train-mode (dropout on: residual 0.3, attention 0.1) gradient vs a central finite difference
+    of the same dropout masks (RNG reset before each forward), along a random direction over every
+    parameter.  Every FFN-up bias is shifted by +8 so each ReLU stays active and the loss is smooth:
+    with the fixture's biases a +-1e-3 step moves pre-activations across ReLU kinks and the central
+    difference itself is off by 1-30 % depending on the masks (tools/fd_probe.py: the same 5 % even
+    with both dropouts off), which says nothing about the masks.  Smooth, it agrees to < 0.15 % for
+    every seed measured; a backward regenerating any mask differently from its forward would not."""
     cfg, seed, z = load_fixture("c1")
     cfg = cfg.replace(dropout=0.3)
     e = _engine(cfg, seed)
-    f, p, c = _inputs(z)
     sd = e.state_dict(with_buffer=False)
-    e.set_rng_seed(7)
+    for k in sd:
+        if k.endswith("position_wise_1.bias"):
+            sd[k] = sd[k] + 8.0
+    e.load_state_dict(sd)
+    f, p, c = _inputs(z)
+    e.set_rng_seed(rng_seed)
     e.forward(f, p, c)
     e.backward()
     g = e.grads_state_dict()
@@ -683,13 +693,13 @@ def test_dropout_backward_directional_derivative_fp32():
 
     def loss_at(sign):
         e.load_state_dict({k: sd[k] + sign * eps * direction[k] for k in sd})
-        e.set_rng_seed(7)
+        e.set_rng_seed(rng_seed)
         out = e.forward(f, p, c)
         torch.cuda.synchronize()
         return out.item()
 
     numeric = (loss_at(1) - loss_at(-1)) / (2 * eps)
-    assert abs(numeric - analytic) <= 2e-2 * abs(analytic) + 1e-3, (numeric, analytic)
+    assert abs(numeric - analytic) <= 5e-3 * abs(analytic) + 1e-4, (numeric, analytic)
 
 
 @pytest.mark.parametrize("in_dt", ["fp32", "bf16"])

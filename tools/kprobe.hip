@@ -162,6 +162,37 @@ int main() {
           CK(hipStreamWriteValue32(s, sig, (uint32_t)i, 0));
         }
       }) / K);
+      // a fork per kernel to a second stream (the engine's per-block flush): event record + wait vs
+      // a memory write + a wait-on-value packet; the signalling stream's time per kernel
+      hipEvent_t enf;
+      CK(hipEventCreateWithFlags(&enf, hipEventDisableTiming | hipEventDisableSystemFence));
+      std::printf("fork event (no system fence)     : %.2f us/iter\n", time_it(s, 3, [&] {
+        for (int i = 0; i < K; ++i) {
+          tiny<<<1024, 256, 0, s>>>(p);
+          CK(hipEventRecord(enf, s));
+          CK(hipStreamWaitEvent(s2, enf, 0));
+          tiny<<<64, 256, 0, s2>>>(p + 64);
+        }
+      }) / K);
+      CK(hipDeviceSynchronize());
+      uint32_t seq = 1u << 20;
+      std::printf("fork writeValue/waitValue        : %.2f us/iter\n", time_it(s, 3, [&] {
+        for (int i = 0; i < K; ++i) {
+          tiny<<<1024, 256, 0, s>>>(p);
+          ++seq;
+          CK(hipStreamWriteValue32(s, sig + 16, seq, 0));
+          CK(hipStreamWaitValue32(s2, sig + 16, seq, hipStreamWaitValueGte, 0xFFFFFFFFu));
+          tiny<<<64, 256, 0, s2>>>(p + 64);
+        }
+      }) / K);
+      CK(hipDeviceSynchronize());
+      std::printf("no fork (same kernels, s2 free)  : %.2f us/iter\n", time_it(s, 3, [&] {
+        for (int i = 0; i < K; ++i) {
+          tiny<<<1024, 256, 0, s>>>(p);
+          tiny<<<64, 256, 0, s2>>>(p + 64);
+        }
+      }) / K);
+      CK(hipDeviceSynchronize());
     } else {
       std::printf("signal memory unavailable\n");
     }
