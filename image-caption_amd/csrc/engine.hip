@@ -217,6 +217,42 @@ struct capgen_engine {
         else if (!trans_only) qkv_tile_weights(shadow + kv.first, kv.second.second, 512, wtile + kv.second.first, s);
       }
   }
+  // bf16 decode: the decoder Linears as MFMA fragment pieces for the register-B GEMM (gemm_breg.hip,
+  // CAPGEN_BREG_DECODE, default on).  Wqkv / Wq_c are the fronts' tiles (the same layout at K = 512);
+  // the others (Wo_s, Wo_c, W1, W2, the word-embedding projection) are rebuilt from the bf16 shadow at
+  // the start of every greedy / beam call -- ~30 MB at C4, the weights may have moved since the last one
+  bool breg_decode_on = knob(Knob::BregDecode) != 0;
+  bf16* dtiles = nullptr;
+  std::map<int64_t, int64_t> dtile;  // arena offset -> element offset in dtiles
+  std::vector<std::array<int64_t, 3>> dtile_list() const {  // {arena offset, rows N, columns K}
+    std::vector<std::array<int64_t, 3>> v;
+    v.push_back({L.Wel, L.dd, L.dwe});
+    for (const auto& e : L.dec)
+      v.push_back({e.Wo_s, L.dd, L.dd}), v.push_back({e.Wo_c, L.dd, L.dd}), v.push_back({e.W1, L.fd, L.dd}),
+          v.push_back({e.W2, L.dd, L.fd});
+    return v;
+  }
+  bool breg_decode() const { return breg_decode_on && act == DType::BF16; }
+  const void* DT(int64_t off) const {
+    if (!breg_decode()) return nullptr;
+    if (const bf16* t = WT(off)) return t;
+    auto it = dtile.find(off);
+    return it == dtile.end() || !dtiles ? nullptr : dtiles + it->second;
+  }
+  void ensure_dtiles() {  // (outside any capture)
+    if (dtiles || !breg_decode()) return;
+    int64_t tot = 0;
+    for (const auto& t : dtile_list())
+      if (t[1] % 16 == 0 && t[2] % 32 == 0) dtile[t[0]] = tot, tot += t[1] * t[2];
+    if (tot) CAPGEN_HIP(hipMalloc(&dtiles, (size_t)tot * 2));
+  }
+  void build_dtiles(hipStream_t s) {
+    if (!dtiles) return;
+    for (const auto& t : dtile_list()) {
+      auto it = dtile.find(t[0]);
+      if (it != dtile.end()) gemm_tile_b(shadow + t[0], t[2], 0, (int)t[1], (int)t[2], dtiles + it->second, s);
+    }
+  }
   float* pe = nullptr;  // [max_length-1, dd] f32 sinusoid table
   int64_t* step = nullptr;
   float* adam_scal = nullptr;
@@ -451,10 +487,12 @@ struct capgen_engine {
   }
 
   // C[M,N] = A[M,K] . W[N,K]^T  (nn.Linear)
+  // bt: the weight's fragment pieces (DT), read by the register-B GEMM where it takes the shape
   void linear(const void* X, int64_t ldx, int64_t woff, int64_t ldw, void* C, int64_t ldc, DType tout, int M,
-              int N, int K, const float* bias, int relu, hipStream_t s) {
+              int N, int K, const float* bias, int relu, hipStream_t s, const void* bt = nullptr) {
     GemmArgs ga;
     ga.M = M, ga.N = N, ga.K = K, ga.A = X, ga.lda = ldx, ga.B = W(woff), ga.ldb = ldw, ga.C = C, ga.ldc = ldc;
+    ga.bt = bt;
     ga.bias = bias;
     ga.relu = relu;
     ga.prio = prio(s);
@@ -1800,7 +1838,7 @@ struct capgen_engine {
                 const int32_t* kv_row = nullptr) {
     const int dd = L.dd, Hd = L.Hd, dkd = dd / Hd, Tc = L.maxlen;
     embedding_gather(P(L.emb), ids + t, Tc, R, L.dwe, g.E, act, s, L.V);
-    linear(g.E, L.dwe, L.Wel, L.dwe, g.tmp, dd, act, R, dd, L.dwe, nullptr, 0, s);
+    linear(g.E, L.dwe, L.Wel, L.dwe, g.tmp, dd, act, R, dd, L.dwe, nullptr, 0, s, DT(L.Wel));
     LnFwd ln;
     ln.M = R, ln.d = dd, ln.a = g.tmp, ln.pe = pe + (int64_t)t * dd, ln.pe_L = 1, ln.gamma = P(L.dec_lng);
     ln.beta = P(L.dec_lnb), ln.y = g.x;
@@ -1815,6 +1853,7 @@ struct capgen_engine {
         GemmArgs ga;
         ga.M = R, ga.N = 3 * dd, ga.K = dd, ga.A = g.x, ga.lda = dd, ga.B = W(w.Wqkv), ga.ldb = dd;
         ga.C = g.q, ga.ldc = dd, ga.C2 = at(cl, (int64_t)t * 2 * dd), ga.ldc2 = cld, ga.nsplit = dd;
+        ga.bt = DT(w.Wqkv);
         gemm(ga, act, act, false, false, s);
       } else {
         linear(g.x, dd, w.Wqkv, dd, g.q, dd, act, R, dd, dd, nullptr, 0, s);
@@ -1831,12 +1870,12 @@ struct capgen_engine {
       sg.kv_row = kv_row, sg.kv_row_ld = Tc;
       sg.temperature = std::sqrt((float)dkd);
       attf(sg, g.att, nullptr, act, s);
-      linear(g.att, dd, w.Wo_s, dd, g.tmp, dd, act, R, dd, dd, nullptr, 0, s);
+      linear(g.att, dd, w.Wo_s, dd, g.tmp, dd, act, R, dd, dd, nullptr, 0, s, DT(w.Wo_s));
       LnFwd l1;
       l1.M = R, l1.d = dd, l1.a = g.tmp, l1.res = g.x, l1.gamma = P(w.lsg), l1.beta = P(w.lsb), l1.y = g.x1;
       lnf(l1, s);
       const bool want_p = want_attn && l == L.Ld - 1;
-      linear(g.x1, dd, w.Wq_c, dd, g.q, dd, act, R, dd, dd, nullptr, 0, s);
+      linear(g.x1, dd, w.Wq_c, dd, g.q, dd, act, R, dd, dd, nullptr, 0, s, DT(w.Wq_c));
       AttnGeom c;  // rows r -> image r % Bimg
       c.H = Hd, c.Lk = N, c.dk = dkd;
       c.k = at(a.KV, (int64_t)l * 2 * dd), c.k_ld = kvld, c.k_bs = (int64_t)N * kvld;
@@ -1857,12 +1896,12 @@ struct capgen_engine {
         c.o_ld = dd, c.o_bs = dd;
       }
       attf(c, g.att, want_p ? g.Pc : nullptr, act, s);
-      linear(g.att, dd, w.Wo_c, dd, g.tmp, dd, act, R, dd, dd, nullptr, 0, s);
+      linear(g.att, dd, w.Wo_c, dd, g.tmp, dd, act, R, dd, dd, nullptr, 0, s, DT(w.Wo_c));
       LnFwd l2;
       l2.M = R, l2.d = dd, l2.a = g.tmp, l2.res = g.x1, l2.gamma = P(w.lcg), l2.beta = P(w.lcb), l2.y = g.x2;
       lnf(l2, s);
-      linear(g.x2, dd, w.W1, dd, g.h, L.fd, act, R, L.fd, dd, P(w.b1), 1, s);
-      linear(g.h, L.fd, w.W2, L.fd, g.tmp, dd, act, R, dd, L.fd, nullptr, 0, s);
+      linear(g.x2, dd, w.W1, dd, g.h, L.fd, act, R, L.fd, dd, P(w.b1), 1, s, DT(w.W1));
+      linear(g.h, L.fd, w.W2, L.fd, g.tmp, dd, act, R, dd, L.fd, nullptr, 0, s, DT(w.W2));
       LnFwd l3;
       l3.M = R, l3.d = dd, l3.a = g.tmp, l3.a_bias = P(w.b2), l3.res = g.x2, l3.gamma = P(w.lfg), l3.beta = P(w.lfb);
       l3.mask = rm, l3.y = g.x;
@@ -1898,6 +1937,7 @@ struct capgen_engine {
     require(B >= 1, "greedy: need B >= 1");
     ensure_acts(B, N, 2);
     ensure_gen(B, N);
+    ensure_dtiles();
     const GenKey key{(attn_out ? 1 : 0) + (decode_logsm ? 8 : 0), feats, pos, (int)ft, B, N, 0};
     gen_run(key, [&] { greedy_body(feats, ft, pos, B, N, g.out_ids, attn_out ? g.out_attn : nullptr, s); }, s);
     CAPGEN_HIP(hipMemcpyAsync(ids_out, g.out_ids, sizeof(int64_t) * B * (L.maxlen + 1), hipMemcpyDeviceToDevice, s));
@@ -1909,6 +1949,7 @@ struct capgen_engine {
                    hipStream_t s) {
     encode_only(feats, ft, pos, B, N, s);
     ensure_gen(B, N);
+    build_dtiles(s);
     const int Tc = L.maxlen, W = L.maxlen + 1;
     init_gen_ids_kernel<<<(B * std::max(W, Tc) + 255) / 256, 256, 0, s>>>(ids_out, B, W, g.ids, Tc);
     CAPGEN_HIP(hipGetLastError());
@@ -1928,6 +1969,7 @@ struct capgen_engine {
     require(B >= 1 && N >= 1 && N <= 64, "beam_search: need B >= 1 and N in [1, 64]");
     ensure_acts(B, N, 2);
     ensure_gen(k * B, N);
+    ensure_dtiles();
     const GenKey key{2 + (decode_logsm ? 8 : 0), feats, pos, (int)ft, B, N, k};
     gen_run(key, [&] { beam_body(feats, ft, pos, B, N, k, g.out_ids, s); }, s);
     CAPGEN_HIP(hipMemcpyAsync(ids_out, g.out_ids, sizeof(int64_t) * B * L.maxlen, hipMemcpyDeviceToDevice, s));
@@ -1936,6 +1978,7 @@ struct capgen_engine {
     const int R = k * B, Tc = L.maxlen, Tw = L.maxlen, dd = L.dd;
     encode_only(feats, ft, pos, B, N, s);
     ensure_gen(R, N);
+    build_dtiles(s);
     init_gen_ids_kernel<<<(R * Tc + 255) / 256, 256, 0, s>>>(g.seq, R, Tw, g.ids, Tc);
     CAPGEN_HIP(hipGetLastError());
     // position 0: every beam holds <START>; top-k of beam 0's distribution (model.py:148-166)
@@ -1980,7 +2023,7 @@ struct capgen_engine {
     if (es) (void)hipStreamSynchronize(es);
     drop_graph();
     if (comm) ncclCommDestroy(comm);
-    for (void* p : {(void*)params, (void*)grads, (void*)am, (void*)av, (void*)shadow, (void*)wtile, (void*)pe, (void*)step,
+    for (void* p : {(void*)params, (void*)grads, (void*)am, (void*)av, (void*)shadow, (void*)wtile, (void*)dtiles, (void*)pe, (void*)step,
                     (void*)adam_scal, (void*)seed, (void*)scalars, (void*)gstripe, ws, gws, (void*)stamp_ring})
       if (p) (void)hipFree(p);
     if (count_host) (void)hipHostFree(count_host);
@@ -2352,6 +2395,21 @@ int capgen_debug_gemm(int M, int N, int K, const void* A, int64_t lda, int ta, c
     ga.M = M, ga.N = N, ga.K = K, ga.A = A, ga.lda = lda, ga.B = B, ga.ldb = ldb, ga.C = Cp, ga.ldc = ldc;
     ga.bias = bias, ga.alpha = alpha, ga.beta = beta, ga.relu = relu;
     gemm(ga, dt(in_dtype), dt(out_dtype), ta != 0, tb != 0, (hipStream_t)stream);
+  });
+}
+
+int capgen_debug_gemm_tiled(int M, int N, int K, const void* A, int64_t lda, const void* B, int64_t ldb, int tb,
+                            void* Bt, void* Cp, int64_t ldc, int out_dtype, const float* bias, int beta, int relu,
+                            const void* aux, int64_t ldaux, void* stream) {
+  return guarded([&] {
+    gemm_init();
+    const hipStream_t s = (hipStream_t)stream;
+    gemm_tile_b(reinterpret_cast<const bf16*>(B), ldb, tb, N, K, reinterpret_cast<bf16*>(Bt), s);
+    GemmArgs ga;
+    ga.M = M, ga.N = N, ga.K = K, ga.A = A, ga.lda = lda, ga.B = B, ga.ldb = ldb, ga.C = Cp, ga.ldc = ldc;
+    ga.bias = bias, ga.beta = beta, ga.relu = relu, ga.aux = aux, ga.ldaux = ldaux, ga.bt = Bt;
+    require(gemm_breg_ok(ga), "debug_gemm_tiled: a shape / epilogue the register-B kernel does not take");
+    gemm(ga, DType::BF16, dt(out_dtype), false, tb != 0, s);
   });
 }
 

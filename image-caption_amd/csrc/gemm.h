@@ -28,8 +28,8 @@ struct GemmArgs {
   const float* alpha_ptr = nullptr;  // device scalar multiplied into alpha (e.g. 1/count)
   int beta = 0;                      // 1: accumulate into C
   int prio = 0;                      // 1: critical-path launch, waves raise their issue priority
-  const float* cin = nullptr;        // unsupported (must stay null; kept so the argument layout is unchanged)
-  int64_t ldcin = 0;
+  const void* bt = nullptr;          // bf16: B's MFMA fragment pieces (gemm_tile_b) -> the register-B
+  int64_t bt_pad_ = 0;               //   path (gemm_breg.hip) where it takes the shape; null: the LDS ring
   void* C2 = nullptr;                // bf16 path: columns n >= nsplit go to C2[m][n - nsplit] (row
   int64_t ldc2 = 0;                  //   stride ldc2), e.g. Q to one buffer and K/V to a cache
   int nsplit = 0;                    //   (nsplit % 4 == 0)
@@ -70,6 +70,13 @@ static_assert(sizeof(GemmGroup) == 4 * (1 + 2 * kMaxGroup + 1) + kMaxGroup * siz
 
 // ta: A stored [K][M] (else [M][K]); tb: B stored [K][N] (else [N][K]).
 void gemm(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t s);
+// gemm_breg.hip: the bf16 GEMM reading B from its fragment pieces g.bt (A stored [M][K]).
+// gemm_tile_b writes the pieces of B (stored [N][K] for tb = 0, [K][N] for tb = 1; N % 16 == 0,
+// K % 32 == 0) into Bt (N * K bf16): piece (j, ks) = 512 bf16, lane l holding B[32 ks + 8 (l >> 4) + e]
+// [16 j + (l & 15)] for e = 0..7.
+bool gemm_breg_ok(const GemmArgs& g);
+void gemm_breg(const GemmArgs& g, DType out, hipStream_t s);
+void gemm_tile_b(const bf16* B, int64_t ldb, int tb, int N, int K, bf16* Bt, hipStream_t s);
 // allocate the per-device zero page used for out-of-range tiles (call before any bf16 gemm,
 // outside graph capture)
 void gemm_init();

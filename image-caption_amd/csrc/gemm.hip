@@ -258,7 +258,7 @@ void gemm_hz_regions(const GemmArgs& g, DType in, DType out, bool ta, bool tb, s
   if (g.beta) v.push_back(blk(g.C, g.M, ncol * eo, g.ldc * eo, RD));
   if (g.C2) v.push_back(blk(g.C2, g.M, (int64_t)(g.N - g.nsplit) * eo, g.ldc2 * eo, WR));
   v.push_back(blk(g.aux, g.M, g.N * ei, g.ldaux * ei, RD));
-  v.push_back(blk(g.cin, g.M, g.N * 4, g.ldcin * 4, RD));
+  v.push_back(rd(g.bt, (int64_t)g.N * g.K * 2));
   v.push_back(rd(g.bias, g.N * 4));
   v.push_back(rd(g.alpha_ptr, 4));
   v.push_back(blk(g.colsum, g.colsum_stripes, g.N * 4, g.colsum_stride * 4, ACC));
@@ -293,7 +293,7 @@ static void gemm_impl(const GemmArgs& g, DType in, DType out, bool ta, bool tb, 
   require(((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0, "gemm: operands must be 16-B aligned");
   require(g.K > 0, "gemm: K must be positive");
   require(!g.colsum || !g.beta, "gemm: colsum requires beta == 0");
-  require(!g.cin, "gemm: the cin epilogue input is not supported (removed with its only user)");
+  require(!g.bt || (in == DType::BF16 && !ta), "gemm: a tiled B (bt) needs the bf16 path with A stored [M][K]");
   require(!g.dec_stats || in == DType::BF16, "gemm: dec_stats is a bf16-path epilogue output");
   require(!g.C2 || (in == DType::BF16 && g.nsplit % 4 == 0 && !g.beta && !g.colsum),
           "gemm: a split output (C2) needs the bf16 path, nsplit % 4 == 0, no beta / colsum");

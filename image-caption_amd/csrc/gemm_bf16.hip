@@ -742,11 +742,15 @@ void gemm_bf16(const GemmArgs& g_in, DType out, bool ta, bool tb, hipStream_t s)
   require(!g.beta || (((uintptr_t)g.C & 127) == 0 && (g.ldc * (int64_t)dsize(out)) % 128 == 0),
           "gemm(bf16): beta=1 needs C rows 128-B aligned (one writer per cache line)");
   require(!g.ce_stats || (out == DType::BF16 && !ta && !tb && !g.beta && !g.C2 && !g.aux && !g.relu && !g.colsum &&
-                          !g.cin && g.ce_tgt && g.ce_tlogit && g.ce_ld >= (g.N + 15) / 16),
+                          g.ce_tgt && g.ce_tlogit && g.ce_ld >= (g.N + 15) / 16),
           "gemm(bf16): the fused cross-entropy epilogue is a plain bf16 NT GEMM (+bias)");
   require(!g.dec_stats || (out == DType::F32 && !ta && !tb && !g.beta && !g.C2 && !g.aux && !g.relu && !g.colsum &&
-                           !g.cin && !g.ce_stats && g.dec_ld >= (g.N + 15) / 16),
+                           !g.ce_stats && g.dec_ld >= (g.N + 15) / 16),
           "gemm(bf16): the decode slab-stats epilogue is a plain f32-out NT GEMM (+bias)");
+  if (!ta && g.bt && gemm_breg_ok(g)) {  // B handed over as fragment pieces: the register-B kernel
+    gemm_breg(g, out, s);
+    return;
+  }
   if (out == DType::F32) launch_bf16_layout<float>(g, ta, tb, s);
   else launch_bf16_layout<bf16>(g, ta, tb, s);
 }

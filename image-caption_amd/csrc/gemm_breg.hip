@@ -1,0 +1,197 @@
+// capgen — bf16 GEMM with the B operand streamed into registers from a tiled copy (round 5).
+//
+// C[M,N] = A[M,K] . B[K,N] where B is handed over as its MFMA fragments: piece (j, ks) is 512 bf16,
+// lane l holding B[32 ks + 8 (l >> 4) + e][16 j + (l & 15)], e = 0..7 -- the B fragment of
+// v_mfma_f32_16x16x32_bf16 for column block j and 32-deep k-step ks, one coalesced 1-KB load
+// (gemm_tile_b builds it from B stored [N][K] (nn.Linear weights, the forward) or [K][N]).
+//
+// The form of the attention fronts (qkv_attn.hip), measured against the LDS-DMA ring of gemm_tile.h
+// by tools/breg_probe.hip (kernel durations under rocprofv3, `profiles/r05_breg_probe.txt`): the
+// 4 waves of a workgroup split N, so each wave's weight fragments are private to it and go straight
+// from L2 into a double-buffered register batch of QB k-steps; only the A rows (shared by the waves)
+// pass through LDS -- a 2-stage ring filled from registers AD k-tiles ahead (plain loads and
+// ds_write_b128: every wait is hipcc's own).  No ring DMA issue, no per-k-tile B fragment reads: at
+// the decode step's shapes (M = 256 / 1280 rows, K = 512) 27-38 % below the ring's kernel time,
+// 6-12 % at K = 2048.
+//
+// Tile: BM x BN, wave w = all BM rows x columns [w BN/4, (w+1) BN/4); A k-tiles of 32 KT; tiles are
+// grouped per XCD (XCD x = blockIdx % 8 takes the x-th contiguous chunk of the M-major tile list:
+// its tiles share A row panels).  The epilogue is gemm_tile.h's (bias, ReLU, ReLU' mask, beta, split
+// output C2): lane holds C[m0 + 16 i + (l & 15)][n0 + w BN/4 + 16 f + 4 (l >> 4) + 0..3].
+#include <type_traits>
+
+#include "gemm_tile.h"
+#include "hazard.h"
+
+namespace capgen {
+namespace {
+
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
+template <typename TO, int BM, int BN, int QB, int AD, int KT>
+__global__ void __launch_bounds__(256) breg_kernel(GemmArgs g) {
+  constexpr int FM = BM / 16, WN = BN / 4, FN = WN / 16;
+  constexpr int TPB = QB / KT;            // k-tiles per B batch
+  constexpr int CPT = BM * KT * 4 / 256;  // 16-B A chunks per thread per k-tile
+  constexpr int RB = KT * 64;             // LDS bytes per A row per stage
+  static_assert(TPB % AD == 0 && AD % 2 == 0 && CPT >= 1 && FN >= 1, "breg tile shape");
+  __shared__ __attribute__((aligned(16))) char sA[2][BM * RB];
+  StampScope stamp_scope(g.stamp);
+  if (g.prio) __builtin_amdgcn_s_setprio(3);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int M = g.M, N = g.N, K = g.K;
+  const int MT = (M + BM - 1) / BM, NT = N / BN, T = MT * NT;
+  const int per = (T + 7) / 8;
+  const int tile = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (tile >= T) return;
+  const int mt = tile / NT, nt = tile % NT;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int nk = K / (32 * KT), nb = K / (32 * QB), KS = K / 32;
+  const bf16* __restrict__ A = reinterpret_cast<const bf16*>(g.A);
+  const bf16* __restrict__ Bt = reinterpret_cast<const bf16*>(g.bt);
+
+  const bf16* brow[FN];
+#pragma unroll
+  for (int f = 0; f < FN; ++f) brow[f] = Bt + ((int64_t)((n0 + w * WN) / 16 + f) * KS * 64 + lane) * 8;
+  bf16x8 bq[2][QB][FN];
+  auto loadB = [&](int b, bf16x8 (&dst)[QB][FN]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < QB; ++q)
+#pragma unroll
+      for (int f = 0; f < FN; ++f) dst[q][f] = *reinterpret_cast<const bf16x8*>(brow[f] + (int64_t)(b * QB + q) * 512);
+  };
+  // A rows past M read row M - 1 (their results are never stored)
+  const bf16* arow[CPT];
+  int aoff[CPT];
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int id = tid + 256 * c, row = id / (KT * 4), ch = id % (KT * 4);
+    arow[c] = A + (int64_t)min(m0 + row, M - 1) * g.lda + ch * 8;
+    aoff[c] = row * RB + ((ch ^ (row & 7)) * 16);
+  }
+  u32x4 ar[AD][CPT];  // A(t) in ar[t % AD], loaded AD - 1 k-tiles before its LDS write
+  auto loadA = [&](int kt, u32x4 (&r)[CPT]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) r[c] = *reinterpret_cast<const u32x4*>(arow[c] + kt * KT * 32);
+  };
+  auto writeA = [&](int st, const u32x4 (&r)[CPT]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) *reinterpret_cast<u32x4*>(sA[st] + aoff[c]) = r[c];
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int f = 0; f < FN; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int i = 0; i < AD; ++i)
+    if (i < nk) loadA(i, ar[i]);
+  loadB(0, bq[0]);
+  if (nb > 1) loadB(1, bq[1]);
+  writeA(0, ar[0]);
+  if (AD < nk) loadA(AD, ar[0]);
+
+  // one B batch (TPB k-tiles) from register buffer H (a compile-time index: a runtime one sends the
+  // batches to scratch)
+  auto batch = [&](int b, auto Hc) __attribute__((always_inline)) {
+    constexpr int H = decltype(Hc)::value;
+#pragma unroll
+    for (int tt = 0; tt < TPB; ++tt) {
+      const int t = b * TPB + tt;  // t % AD == tt % AD: TPB is a multiple of AD
+      __syncthreads();             // A(t) visible in stage t & 1; stage (t + 1) & 1 free
+      if (t + 1 < nk) {
+        writeA((tt + 1) & 1, ar[(tt + 1) % AD]);
+        if (t + 1 + AD < nk) loadA(t + 1 + AD, ar[(tt + 1) % AD]);
+      }
+      const char* st = sA[tt & 1];
+#pragma unroll
+      for (int ks = 0; ks < KT; ++ks) {
+        bf16x8 af[FM];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int row = 16 * i + (lane & 15), ch = 4 * ks + (lane >> 4);
+          af[i] = *reinterpret_cast<const bf16x8*>(st + row * RB + ((ch ^ (row & 7)) * 16));
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int f = 0; f < FN; ++f)
+            acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[H][KT * tt + ks][f], af[i], acc[i][f], 0, 0, 0);
+      }
+    }
+    if (b + 2 < nb) loadB(b + 2, bq[H]);
+  };
+  for (int bb = 0; bb < nb; bb += 2) {
+    batch(bb, std::integral_constant<int, 0>{});
+    if (bb + 1 < nb) batch(bb + 1, std::integral_constant<int, 1>{});
+  }
+  const float alpha = g.alpha_ptr ? g.alpha * *g.alpha_ptr : g.alpha;
+  tile_epilogue<TO, FM, FN, BM, WN>(g, acc, m0, n0, 0, w, lane, alpha, 0, 1);
+}
+
+// B[k][n] of B stored [N][K] (tb = 0) or [K][N] (tb = 1) -> the fragment pieces: one thread per
+// (piece, lane) writes 16 B; the [N][K] form reads 16 contiguous bytes, the [K][N] form 8 strided bf16
+__global__ void tile_b_kernel(const bf16* __restrict__ B, int64_t ldb, int tb, int N, int K, bf16* __restrict__ Bt) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int KS = K / 32;
+  if (i >= (int64_t)(N / 16) * KS * 64) return;
+  const int lane = (int)(i & 63);
+  const int64_t p = i >> 6;
+  const int j = (int)(p / KS), ks = (int)(p % KS);
+  const int n = 16 * j + (lane & 15), k0 = 32 * ks + 8 * (lane >> 4);
+  bf16x8 v;
+  if (tb) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = B[(int64_t)(k0 + e) * ldb + n];
+  } else {
+    v = *reinterpret_cast<const bf16x8*>(B + (int64_t)n * ldb + k0);
+  }
+  *reinterpret_cast<bf16x8*>(Bt + i * 8) = v;
+}
+
+template <typename TO, int BM, int BN, int QB, int AD, int KT>
+void launch(const GemmArgs& g, hipStream_t s) {
+  const int T = ((g.M + BM - 1) / BM) * (g.N / BN);
+  breg_kernel<TO, BM, BN, QB, AD, KT><<<((T + 7) / 8) * 8, 256, 0, s>>>(g);
+}
+
+}  // namespace
+
+// the launch choice (tools/breg_probe.hip, kernel durations): 64 x 64 tiles with 4-step batches for
+// wide outputs at >= 1024 rows, else 32 x 64 tiles, 128-deep k-tiles and 8-step batches
+static bool breg_wide(const GemmArgs& g) { return g.N >= 1536 && g.M >= 1024; }
+
+bool gemm_breg_ok(const GemmArgs& g) {
+  const int kq = breg_wide(g) ? 128 : 256;  // 32 * QB
+  return g.bt && g.M >= 1 && g.N % 64 == 0 && g.K >= kq && g.K % kq == 0 && g.lda % 8 == 0 &&
+         ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.bt & 15) == 0 && !g.ce_stats && !g.dec_stats && !g.colsum;
+}
+
+void gemm_breg(const GemmArgs& g, DType out, hipStream_t s) {
+  require(gemm_breg_ok(g), "gemm_breg: unsupported shape or epilogue");
+  const bool wide = breg_wide(g);
+  if (out == DType::BF16) {
+    if (wide) launch<bf16, 64, 64, 4, 2, 2>(g, s);
+    else launch<bf16, 32, 64, 8, 2, 4>(g, s);
+  } else {
+    if (wide) launch<float, 64, 64, 4, 2, 2>(g, s);
+    else launch<float, 32, 64, 8, 2, 4>(g, s);
+  }
+}
+
+void gemm_tile_b(const bf16* B, int64_t ldb, int tb, int N, int K, bf16* Bt, hipStream_t s) {
+  require(N % 16 == 0 && K % 32 == 0 && ldb % 8 == 0, "gemm_tile_b: N % 16, K % 32, ldb % 8");
+  if (hz::active()) {
+    using namespace hz;
+    op(s, "gemm_tile_b", {tb ? blk(B, K, (int64_t)N * 2, ldb * 2, RD) : blk(B, N, (int64_t)K * 2, ldb * 2, RD),
+                          wr(Bt, (int64_t)N * K * 2)});
+  }
+  const int64_t thr = (int64_t)(N / 16) * (K / 32) * 64;
+  tile_b_kernel<<<(unsigned)((thr + 255) / 256), 256, 0, s>>>(B, ldb, tb, N, K, Bt);
+  CAPGEN_HIP(hipGetLastError());
+}
+
+}  // namespace capgen

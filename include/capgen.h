@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define CAPGEN_ABI_VERSION 9
+#define CAPGEN_ABI_VERSION 10
 
 typedef struct capgen_engine capgen_t;
 
@@ -149,6 +149,14 @@ int capgen_set_rng_seed(capgen_t* h, uint64_t seed);
 int capgen_debug_gemm(int M, int N, int K, const void* A, int64_t lda, int ta, const void* B, int64_t ldb, int tb,
                       void* C, int64_t ldc, int in_dtype, int out_dtype, const float* bias, float alpha, int beta,
                       int relu, void* stream);
+
+/* Kernel test hook for the register-B GEMM (gemm_breg.hip, the bf16 decode step's Linears): writes
+ * B's MFMA fragment pieces into Bt (N * K bf16; B stored [K][N] if tb else [N][K]), then
+ * C[M,N] = A[M,K] . B (+bias)(relu)(zeroed where aux <= 0)(+C if beta) on that kernel; fails if the
+ * shape / epilogue is one the kernel does not take (N % 64, K % 256 -- K % 128 at N >= 1536, M >= 1024). */
+int capgen_debug_gemm_tiled(int M, int N, int K, const void* A, int64_t lda, const void* B, int64_t ldb, int tb,
+                            void* Bt, void* C, int64_t ldc, int out_dtype, const float* bias, int beta, int relu,
+                            const void* aux, int64_t ldaux, void* stream);
 
 /* Experiment hook: force a GEMM tile/wave/pipeline variant (0 = production heuristic). */
 int capgen_debug_gemm_variant(int variant);

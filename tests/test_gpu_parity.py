@@ -729,6 +729,77 @@ def test_gemm_kernel_vs_torch(in_dt, ta, tb, M, N, K):
     assert (Cd.cpu() - ref).abs().max().item() <= tol
 
 
+@pytest.mark.parametrize("M,N,K", [(1280, 512, 512), (1280, 1536, 512), (1280, 2048, 512), (256, 512, 2048),
+                                   (200, 512, 512), (1093, 2048, 256), (2304, 512, 1536)])
+@pytest.mark.parametrize("tb", [0, 1])
+@pytest.mark.parametrize("epi", ["plain", "bias_relu", "beta_f32", "aux"])
+def test_gemm_register_b_vs_torch(M, N, K, tb, epi):
+    """The register-B GEMM (gemm_breg.hip: B as MFMA fragment pieces built by gemm_tile_b, the bf16
+    decode step's Linears) against torch: both launch forms (64x64 for N >= 1536 at >= 1024 rows,
+    32x64 otherwise), M tails (200, 1093 rows), B stored [N][K] and [K][N], and gemm_tile.h's epilogue
+    forms it uses (bias + ReLU, beta accumulation into f32, the ReLU' mask)."""
+    import ctypes as C
+    from capgen import _lib
+    lib = _lib.load()
+    g = torch.Generator(device="cpu").manual_seed(M + 3 * N + 7 * K + tb)
+    A = torch.randn(M, K, generator=g).bfloat16()
+    Bm = torch.randn(N, K, generator=g).bfloat16()  # nn.Linear [out][in]
+    bias = torch.randn(N, generator=g)
+    aux = torch.randn(M, N, generator=g).bfloat16()
+    c0 = torch.randn(M, N, generator=g)
+    ref = A.float() @ Bm.float().t()
+    out_f32 = epi == "beta_f32"
+    if epi == "bias_relu":
+        ref = torch.relu(ref + bias)
+    elif epi == "beta_f32":
+        ref = ref + c0
+    elif epi == "aux":
+        ref = torch.where(aux.float() > 0, ref, torch.zeros_like(ref))
+    Ad = A.to(DEV)
+    Bd = (Bm.t().contiguous() if tb else Bm).to(DEV)
+    Bt = torch.empty(N * K, dtype=torch.bfloat16, device=DEV)
+    Cd = c0.to(DEV) if out_f32 else torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    bd, auxd = bias.to(DEV), aux.to(DEV)
+    _lib.check(lib.capgen_debug_gemm_tiled(M, N, K, C.c_void_p(Ad.data_ptr()), K, C.c_void_p(Bd.data_ptr()),
+                                           N if tb else K, tb, C.c_void_p(Bt.data_ptr()), C.c_void_p(Cd.data_ptr()), N,
+                                           0 if out_f32 else 1,
+                                           C.c_void_p(bd.data_ptr()) if epi == "bias_relu" else None,
+                                           1 if out_f32 else 0, 1 if epi == "bias_relu" else 0,
+                                           C.c_void_p(auxd.data_ptr()) if epi == "aux" else None, N, None))
+    torch.cuda.synchronize()
+    err = (Cd.float().cpu() - ref).abs().max().item()
+    # f32 out: accumulation-order error only; bf16 out: plus one rounding of the output (2^-9 relative)
+    tol = 2e-3 * np.sqrt(K) if out_f32 else 2e-3 * np.sqrt(K) + 2.0 ** -8 * ref.abs().max().item()
+    assert err <= tol, (err, tol)
+
+
+def test_breg_decode_tracks_ring_decode(set_knob):
+    """bf16 C4-style decode with the decoder Linears on the register-B GEMM (CAPGEN_BREG_DECODE,
+    default on) against the LDS-ring GEMM: the products differ only in summation order inside the
+    MFMA (last-bit roundings), so greedy and beam-5 sequences agree with the ring engine's on >= 90 %
+    of the images and with the fp32 engine's no worse than 5 points below the ring engine's (as
+    test_fused_attention_fronts_track_separate_launches_bf16)."""
+    set_knob("BREG_DECODE", 0)
+    _, cfg, sd, e0, f, p, c = _c2_setup(B=256, dtype="bf16", weights="fixture")
+    set_knob("BREG_DECODE", 1)
+    _, _, _, e1, _, _, _ = _c2_setup(B=256, dtype="bf16", weights="fixture")
+    _, _, _, e32, _, _, _ = _c2_setup(B=256, dtype="fp32", weights="fixture")
+    fd, pd = f.to(DEV), p.to(DEV)
+    for e in (e0, e1, e32):
+        e.set_training(False)
+    fb = fd.bfloat16()
+    agree = lambda a, b: (a == b).all(1).float().mean().item()
+    g32, _ = e32.greedy(fd, pd)
+    i0, _ = e0.greedy(fb, pd)
+    i1, _ = e1.greedy(fb, pd)
+    assert agree(i0, i1) >= 0.9 and agree(i1, g32) >= agree(i0, g32) - 0.05, (agree(i0, i1), agree(i0, g32),
+                                                                              agree(i1, g32))
+    b32 = e32.beam(fd, pd, 5)
+    b0, b1 = e0.beam(fb, pd, 5), e1.beam(fb, pd, 5)
+    assert agree(b0, b1) >= 0.9 and agree(b1, b32) >= agree(b0, b32) - 0.05, (agree(b0, b1), agree(b0, b32),
+                                                                              agree(b1, b32))
+
+
 @pytest.mark.parametrize("variant", list(range(1, 31)) + [206, 303, 403, 612, 813, 1314, 217, 319, 420])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 1)])
 def test_gemm_every_variant_and_splitk(variant, ta, tb):

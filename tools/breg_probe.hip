@@ -213,8 +213,11 @@ static void run(const char* name, int M, int N, int K, const bf16* A, const bf16
 int main() {
   hipStream_t s;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  // the C2 step's input-gradient shapes, then the C4 decode step's (beam 5: 1280 rows, greedy: 256)
   const int shapes[][3] = {{2304, 512, 2048}, {1216, 512, 2048}, {2304, 512, 1536}, {1216, 512, 1536},
-                           {2304, 2048, 512}, {1216, 2048, 512}, {2304, 512, 512}, {1216, 512, 512}};
+                           {2304, 2048, 512}, {1216, 2048, 512}, {2304, 512, 512},  {1216, 512, 512},
+                           {1280, 512, 512},  {1280, 1536, 512}, {1280, 2048, 512}, {1280, 512, 2048},
+                           {256, 512, 512},   {256, 1536, 512},  {256, 2048, 512},  {256, 512, 2048}};
   for (auto& sh : shapes) {
     const int M = sh[0], N = sh[1], K = sh[2];
     bf16 *A, *W, *Bt, *C;
