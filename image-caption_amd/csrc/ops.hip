@@ -263,20 +263,24 @@ void layernorm_fwd(const LnFwd& a_in, DType t, hipStream_t s) {
 
 // 8 rows (waves) per workgroup: half the workgroups -- and half the striped gamma / beta / bias
 // atomics -- of the 4-row form (round 5: 2.699-2.703 vs 2.726-2.757 ms/step, three alternating rounds;
-// the class 119 vs 137 us/step)
+// the class 119 vs 137 us/step; 16 rows per workgroup: 2.711-2.716 vs 2.678-2.707 ms, slower)
 #ifndef CAPGEN_LNB_NT
 #define CAPGEN_LNB_NT 512
 #endif
+template <typename T, int DPL>
+static void ln_bwd_launch(const LnBwd& a, hipStream_t s) {
+  // (the per-wave partial sums take 3 * NT * DPL floats of LDS: the widest rows keep 8 waves)
+  constexpr int NT = DPL * CAPGEN_LNB_NT > 8 * 1024 ? 512 : CAPGEN_LNB_NT, W = NT / 64;  // one row per wave
+  ln_bwd_kernel<T, DPL, NT><<<(a.M + W - 1) / W, NT, 0, s>>>(a);
+}
 template <typename T>
 static void ln_bwd_dispatch(const LnBwd& a, hipStream_t s) {
-  constexpr int NT = CAPGEN_LNB_NT, W = NT / 64;  // one row per wave, no loop
-  dim3 grid((a.M + W - 1) / W);
   switch (a.d / 64) {
-    case 1: ln_bwd_kernel<T, 1, NT><<<grid, NT, 0, s>>>(a); break;
-    case 2: ln_bwd_kernel<T, 2, NT><<<grid, NT, 0, s>>>(a); break;
-    case 4: ln_bwd_kernel<T, 4, NT><<<grid, NT, 0, s>>>(a); break;
-    case 8: ln_bwd_kernel<T, 8, NT><<<grid, NT, 0, s>>>(a); break;
-    case 16: ln_bwd_kernel<T, 16, NT><<<grid, NT, 0, s>>>(a); break;
+    case 1: ln_bwd_launch<T, 1>(a, s); break;
+    case 2: ln_bwd_launch<T, 2>(a, s); break;
+    case 4: ln_bwd_launch<T, 4>(a, s); break;
+    case 8: ln_bwd_launch<T, 8>(a, s); break;
+    case 16: ln_bwd_launch<T, 16>(a, s); break;
     default: throw Error("layernorm: width must be 64 * {1,2,4,8,16}");
   }
 }
