@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CAPGEN_LIB_PATH") or os.path.join(_HERE, "libcapgen.so")  # (diagnostic builds)
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 F32, BF16 = 0, 1
 
@@ -74,6 +74,8 @@ _SIGS = {
                                     _P, C.c_int64, C.c_int, C.c_int, _P, C.c_float, C.c_int, C.c_int, _P]),
     "capgen_debug_gemm_tiled": (C.c_int, [C.c_int, C.c_int, C.c_int, _P, C.c_int64, _P, C.c_int64, C.c_int, _P, _P,
                                           C.c_int64, C.c_int, _P, C.c_int, C.c_int, _P, C.c_int64, _P]),
+    "capgen_debug_gemm_tiled_ln": (C.c_int, [C.c_int, C.c_int, _P, _P, _P, _P, C.c_int, _P, C.c_int, C.c_int, _P, _P,
+                                             _P, _P, C.c_int64, C.c_int, _P]),
     "capgen_debug_gemm_variant": (C.c_int, [C.c_int]),
     "capgen_debug_splitk_protocol": (C.c_int, [C.c_int]),
     "capgen_debug_splitk_diag": (C.c_int, [_P, C.c_int]),

@@ -266,6 +266,10 @@ void gemm_hz_regions(const GemmArgs& g, DType in, DType out, bool ta, bool tb, s
   v.push_back(blk(g.dec_stats, g.M, (int64_t)((g.N + 15) / 16) * 8, g.dec_ld * 8, WR));
   v.push_back(rd(g.ce_tgt, (int64_t)g.M * 4));
   v.push_back(wr(g.ce_tlogit, (int64_t)g.M * 4));
+  v.push_back(rd(g.ln_gamma, g.K * 4));
+  v.push_back(rd(g.ln_beta, g.K * 4));
+  v.push_back(blk(g.ln_ids, g.ln_ids ? g.M : 0, 4, g.ln_ids_ld * 4, RD));
+  v.push_back(wr(g.ln_y, (int64_t)g.M * g.K * 2));
 }
 
 static void gemm_impl(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t s);
@@ -295,6 +299,8 @@ static void gemm_impl(const GemmArgs& g, DType in, DType out, bool ta, bool tb, 
   require(!g.colsum || !g.beta, "gemm: colsum requires beta == 0");
   require(!g.bt || (in == DType::BF16 && !ta), "gemm: a tiled B (bt) needs the bf16 path with A stored [M][K]");
   require(!g.dec_stats || in == DType::BF16, "gemm: dec_stats is a bf16-path epilogue output");
+  require(!g.ln_gamma || (in == DType::BF16 && !ta && !tb && g.bt && gemm_breg_ok(g)),
+          "gemm: a folded LayerNorm (ln_gamma) needs the register-B path (bf16, bt, K = 512)");
   require(!g.C2 || (in == DType::BF16 && g.nsplit % 4 == 0 && !g.beta && !g.colsum),
           "gemm: a split output (C2) needs the bf16 path, nsplit % 4 == 0, no beta / colsum");
   if (hz::active()) {

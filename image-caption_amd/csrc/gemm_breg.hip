@@ -132,6 +132,116 @@ __global__ void __launch_bounds__(256) breg_kernel(GemmArgs g) {
   tile_epilogue<TO, FM, FN, BM, WN>(g, acc, m0, n0, 0, w, lane, alpha, 0, 1);
 }
 
+// The LayerNorm of the decode step folded into its consumer (GemmArgs::ln_gamma; K = 512 = d): A holds
+// the LayerNorm INPUT rows v (the producing GEMM's epilogue already added bias and residual into the
+// residual buffer, beta = 1), so a 32-row tile's whole A block (32 KB) is loaded once, normalised in
+// registers and left in LDS for all 16 k-steps -- the separate LayerNorm launch and its dependent
+// boundary go away.  Half-wave h of wave w owns rows 2 w + h + 8 i (i < 4); its lane c holds columns
+// 16 c .. 16 c + 15 of each, so the row statistics are 5 xor-shuffles.  The workgroups of column tile
+// 0 also store y (the next producer's residual).  B as in breg_kernel: 16 k-steps in two register
+// batches of 8, both issued before the A block.
+constexpr float kLnEps = 1e-6f;  // modules.py:57,105 (ops.hip LN_EPS)
+
+template <typename TO>
+__global__ void __launch_bounds__(256) breg_ln_kernel(GemmArgs g) {
+  constexpr int BM = 32, BN = 64, QB = 8, KD = 512, KS = KD / 32, RB = KD * 2;
+  constexpr int FM = BM / 16, WN = BN / 4;  // one 16-column fragment per wave
+  __shared__ __attribute__((aligned(16))) char sA[BM * RB];
+  StampScope stamp_scope(g.stamp);
+  if (g.prio) __builtin_amdgcn_s_setprio(3);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int M = g.M, N = g.N;
+  const int MT = (M + BM - 1) / BM, NT = N / BN, T = MT * NT;
+  const int per = (T + 7) / 8;
+  const int tile = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (tile >= T) return;
+  const int mt = tile / NT, nt = tile % NT;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const bf16* __restrict__ A = reinterpret_cast<const bf16*>(g.A);
+  const bf16* brow = reinterpret_cast<const bf16*>(g.bt) + ((int64_t)((n0 + w * WN) / 16) * KS * 64 + lane) * 8;
+  bf16x8 bq[2][QB];
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int q = 0; q < QB; ++q) bq[b][q] = *reinterpret_cast<const bf16x8*>(brow + (int64_t)(b * QB + q) * 512);
+
+  const int h = lane >> 5, c = lane & 31;
+  u32x4 av[4][2];
+  int idv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = min(m0 + 2 * w + h + 8 * i, M - 1);
+    const bf16* p = A + (int64_t)m * g.lda + 16 * c;
+    av[i][0] = *reinterpret_cast<const u32x4*>(p);
+    av[i][1] = *reinterpret_cast<const u32x4*>(p + 8);
+    idv[i] = g.ln_ids ? g.ln_ids[(int64_t)m * g.ln_ids_ld] : 0;
+  }
+  float gm[16], bt[16];
+#pragma unroll
+  for (int e = 0; e < 16; e += 4) {
+    const float4 g4 = *reinterpret_cast<const float4*>(g.ln_gamma + 16 * c + e);
+    const float4 b4 = *reinterpret_cast<const float4*>(g.ln_beta + 16 * c + e);
+    gm[e] = g4.x, gm[e + 1] = g4.y, gm[e + 2] = g4.z, gm[e + 3] = g4.w;
+    bt[e] = b4.x, bt[e + 1] = b4.y, bt[e + 2] = b4.z, bt[e + 3] = b4.w;
+  }
+  bf16* __restrict__ Y = reinterpret_cast<bf16*>(g.ln_y);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 2 * w + h + 8 * i;
+    float x[16];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      x[2 * e] = __uint_as_float(av[i][e >> 2][e & 3] << 16);
+      x[2 * e + 1] = __uint_as_float(av[i][e >> 2][e & 3] & 0xffff0000u);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) s += x[e];
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) s += __shfl_xor(s, o, 64);
+    const float mean = s / (float)KD;
+    float q = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const float t = x[e] - mean;
+      q = fmaf(t, t, q);
+    }
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) q += __shfl_xor(q, o, 64);
+    const float rstd = 1.0f / sqrtf(q / (float)KD + kLnEps);
+    const float keep = g.ln_ids && idv[i] == g.ln_pad ? 0.f : 1.f;
+    bf16x8 y[2];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) y[e >> 3][e & 7] = (bf16)(((x[e] - mean) * rstd * gm[e] + bt[e]) * keep);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) *reinterpret_cast<bf16x8*>(sA + r * RB + (((2 * c + k) ^ (r & 7)) * 16)) = y[k];
+    if (nt == 0 && m0 + r < M) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) *reinterpret_cast<bf16x8*>(Y + (int64_t)(m0 + r) * KD + 16 * c + 8 * k) = y[k];
+    }
+  }
+  __syncthreads();
+
+  f32x4 acc[FM][1];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) acc[i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    bf16x8 af[FM];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int row = 16 * i + (lane & 15), ch = 4 * ks + (lane >> 4);
+      af[i] = *reinterpret_cast<const bf16x8*>(sA + row * RB + ((ch ^ (row & 7)) * 16));
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+      acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[ks / QB][ks % QB], af[i], acc[i][0], 0, 0, 0);
+  }
+  const float alpha = g.alpha_ptr ? g.alpha * *g.alpha_ptr : g.alpha;
+  tile_epilogue<TO, FM, 1, BM, WN>(g, acc, m0, n0, 0, w, lane, alpha, 0, 1);
+}
+
 // B[k][n] of B stored [N][K] (tb = 0) or [K][N] (tb = 1) -> the fragment pieces: one thread per
 // (piece, lane) writes 16 B; the [N][K] form reads 16 contiguous bytes, the [K][N] form 8 strided bf16
 __global__ void tile_b_kernel(const bf16* __restrict__ B, int64_t ldb, int tb, int N, int K, bf16* __restrict__ Bt) {
@@ -158,6 +268,12 @@ void launch(const GemmArgs& g, hipStream_t s) {
   breg_kernel<TO, BM, BN, QB, AD, KT><<<((T + 7) / 8) * 8, 256, 0, s>>>(g);
 }
 
+template <typename TO>
+void launch_ln(const GemmArgs& g, hipStream_t s) {
+  const int T = ((g.M + 31) / 32) * (g.N / 64);
+  breg_ln_kernel<TO><<<((T + 7) / 8) * 8, 256, 0, s>>>(g);
+}
+
 }  // namespace
 
 // the launch choice (tools/breg_probe.hip, kernel durations): 64 x 64 tiles with 4-step batches for
@@ -166,12 +282,21 @@ static bool breg_wide(const GemmArgs& g) { return g.N >= 1536 && g.M >= 1024; }
 
 bool gemm_breg_ok(const GemmArgs& g) {
   const int kq = breg_wide(g) ? 128 : 256;  // 32 * QB
+  const bool ln_ok = !g.ln_gamma || (g.K == 512 && g.ln_beta && g.ln_y && g.ln_y != g.A &&
+                                     ((uintptr_t)g.ln_y & 15) == 0 && ((uintptr_t)g.ln_gamma & 15) == 0 &&
+                                     ((uintptr_t)g.ln_beta & 15) == 0);
   return g.bt && g.M >= 1 && g.N % 64 == 0 && g.K >= kq && g.K % kq == 0 && g.lda % 8 == 0 &&
-         ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.bt & 15) == 0 && !g.ce_stats && !g.dec_stats && !g.colsum;
+         ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.bt & 15) == 0 && !g.ce_stats && !g.dec_stats && !g.colsum &&
+         ln_ok;
 }
 
 void gemm_breg(const GemmArgs& g, DType out, hipStream_t s) {
   require(gemm_breg_ok(g), "gemm_breg: unsupported shape or epilogue");
+  if (g.ln_gamma) {
+    if (out == DType::BF16) launch_ln<bf16>(g, s);
+    else launch_ln<float>(g, s);
+    return;
+  }
   const bool wide = breg_wide(g);
   if (out == DType::BF16) {
     if (wide) launch<bf16, 64, 64, 4, 2, 2>(g, s);

@@ -800,6 +800,83 @@ def test_breg_decode_tracks_ring_decode(set_knob):
                                                                               agree(b1, b32))
 
 
+@pytest.mark.parametrize("M,N", [(256, 512), (1280, 2048), (1280, 1536), (200, 512), (37, 1536)])
+@pytest.mark.parametrize("epi", ["plain", "bias_relu_mask", "beta_f32"])
+def test_gemm_folded_layernorm_vs_torch(M, N, epi):
+    """The decode step's LayerNorm folded into the register-B GEMM (gemm_breg.hip breg_ln_kernel,
+    CAPGEN_DECODE_LN_FOLD): A holds LayerNorm inputs v; the kernel normalises them (modules.py:86-90,
+    eps 1e-6, gamma / beta, rows whose token is the pad id zeroed as modules.py:114-120) and multiplies.
+    Against torch: the stored normalised rows y within one bf16 rounding of the f32 LayerNorm, and the
+    product within the register-B test's bound computed on torch's LayerNorm of the same v; M tails."""
+    import ctypes as C
+    from capgen import _lib
+    lib = _lib.load()
+    K = 512
+    g = torch.Generator(device="cpu").manual_seed(M + 5 * N + len(epi))
+    v = (3.0 * torch.randn(M, K, generator=g) + 0.5).bfloat16()
+    gamma, beta = 1.0 + 0.3 * torch.randn(K, generator=g), 0.2 * torch.randn(K, generator=g)
+    Bm = torch.randn(N, K, generator=g).bfloat16()
+    bias = torch.randn(N, generator=g)
+    c0 = torch.randn(M, N, generator=g)
+    ids = torch.randint(0, 4, (M,), generator=g, dtype=torch.int32)  # pad id 0: ~1/4 of the rows
+    masked = epi == "bias_relu_mask"
+    y = torch.nn.functional.layer_norm(v.float(), (K,), gamma, beta, eps=1e-6)
+    if masked:
+        y = y * (ids != 0).float()[:, None]
+    ref = y.bfloat16().float() @ Bm.float().t()
+    out_f32 = epi == "beta_f32"
+    if masked:
+        ref = torch.relu(ref + bias)
+    elif out_f32:
+        ref = ref + c0
+    Bt = torch.empty(N * K, dtype=torch.bfloat16, device=DEV)
+    Cd = c0.to(DEV) if out_f32 else torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    Yd = torch.full((M, K), float("nan"), dtype=torch.bfloat16, device=DEV)
+    vd, Bd, bd, gd, btd, idd = (t.to(DEV) for t in (v, Bm, bias, gamma, beta, ids))
+    _lib.check(lib.capgen_debug_gemm_tiled_ln(M, N, C.c_void_p(vd.data_ptr()), C.c_void_p(Bd.data_ptr()),
+                                              C.c_void_p(Bt.data_ptr()), C.c_void_p(Cd.data_ptr()),
+                                              0 if out_f32 else 1, C.c_void_p(bd.data_ptr()) if masked else None,
+                                              1 if out_f32 else 0, 1 if masked else 0, C.c_void_p(gd.data_ptr()),
+                                              C.c_void_p(btd.data_ptr()), C.c_void_p(Yd.data_ptr()),
+                                              C.c_void_p(idd.data_ptr()) if masked else None, 1, 0, None))
+    torch.cuda.synchronize()
+    yerr = (Yd.float().cpu() - y).abs().max().item()
+    assert yerr <= 2.0 ** -8 * y.abs().max().item() + 1e-4, yerr
+    err = (Cd.float().cpu() - ref).abs().max().item()
+    tol = 2e-3 * np.sqrt(K) if out_f32 else 2e-3 * np.sqrt(K) + 2.0 ** -8 * ref.abs().max().item()
+    # plus the products of the rows whose y rounds differently by one bf16 ulp
+    tol += 2.0 ** -8 * (y.abs() @ Bm.float().abs().t()).max().item() * 0.05
+    assert err <= tol, (err, tol)
+
+
+@pytest.mark.parametrize("fold", [1, 2])
+def test_decode_layernorm_fold_tracks_separate_launches(set_knob, fold):
+    """bf16 C4-style decode with the decoder LayerNorms folded into their consumer GEMMs
+    (CAPGEN_DECODE_LN_FOLD, default on: the producer adds bias + residual in its epilogue and the
+    LayerNorm input is rounded to bf16 once, where the separate launch rounds the GEMM output before
+    the residual add) against the separate LayerNorm launches: greedy and beam-5 sequences agree on
+    >= 90 % of the images and with the fp32 engine's no worse than 5 points below the unfolded engine's."""
+    set_knob("DECODE_LN_FOLD", 0)
+    _, cfg, sd, e0, f, p, c = _c2_setup(B=256, dtype="bf16", weights="fixture")
+    set_knob("DECODE_LN_FOLD", fold)  # 1: folded below 1024 rows (greedy, not beam-5), 2: at any row count
+    _, _, _, e1, _, _, _ = _c2_setup(B=256, dtype="bf16", weights="fixture")
+    _, _, _, e32, _, _, _ = _c2_setup(B=256, dtype="fp32", weights="fixture")
+    fd, pd = f.to(DEV), p.to(DEV)
+    for e in (e0, e1, e32):
+        e.set_training(False)
+    fb = fd.bfloat16()
+    agree = lambda a, b: (a == b).all(1).float().mean().item()
+    g32, _ = e32.greedy(fd, pd)
+    i0, _ = e0.greedy(fb, pd)
+    i1, _ = e1.greedy(fb, pd)
+    assert agree(i0, i1) >= 0.9 and agree(i1, g32) >= agree(i0, g32) - 0.05, (agree(i0, i1), agree(i0, g32),
+                                                                              agree(i1, g32))
+    b32 = e32.beam(fd, pd, 5)
+    b0, b1 = e0.beam(fb, pd, 5), e1.beam(fb, pd, 5)
+    assert agree(b0, b1) >= 0.9 and agree(b1, b32) >= agree(b0, b32) - 0.05, (agree(b0, b1), agree(b0, b32),
+                                                                              agree(b1, b32))
+
+
 @pytest.mark.parametrize("variant", list(range(1, 31)) + [206, 303, 403, 612, 813, 1314, 217, 319, 420])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 1)])
 def test_gemm_every_variant_and_splitk(variant, ta, tb):
