@@ -74,7 +74,7 @@ _SIGS = {
                                     _P, C.c_int64, C.c_int, C.c_int, _P, C.c_float, C.c_int, C.c_int, _P]),
     "capgen_debug_gemm_tiled": (C.c_int, [C.c_int, C.c_int, C.c_int, _P, C.c_int64, _P, C.c_int64, C.c_int, _P, _P,
                                           C.c_int64, C.c_int, _P, C.c_int, C.c_int, _P, C.c_int64, _P]),
-    "capgen_debug_gemm_tiled_ln": (C.c_int, [C.c_int, C.c_int, _P, _P, _P, _P, C.c_int, _P, C.c_int, C.c_int, _P, _P,
+    "capgen_debug_gemm_tiled_ln": (C.c_int, [C.c_int, C.c_int, _P, _P, _P, _P, _P, C.c_int, _P, C.c_int, C.c_int, _P, _P,
                                              _P, _P, C.c_int64, C.c_int, _P]),
     "capgen_debug_gemm_variant": (C.c_int, [C.c_int]),
     "capgen_debug_splitk_protocol": (C.c_int, [C.c_int]),

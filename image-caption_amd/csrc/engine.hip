@@ -1836,10 +1836,10 @@ struct capgen_engine {
   // Leaves logits [R, V] in g.logits; cross-attn probs of the last block in g.Pc if want_attn.
   // bf16 decode: each decoder LayerNorm whose output feeds a register-B GEMM (the cross-query
   // projection, the FFN's first Linear, the next block's QKV projection) runs inside that GEMM
-  // (GemmArgs::ln_gamma, gemm_breg.hip breg_ln_kernel): the producing Linear accumulates into the
-  // residual buffer (beta = 1: v = X . W^T (+ bias) + residual), the consumer normalises its A rows and
-  // its column-tile-0 workgroups store the normalised rows as the next residual.  17 of the 19
-  // LayerNorm launches of a token go away (CAPGEN_DECODE_LN_FOLD=0: separate launches).
+  // (GemmArgs::ln_gamma, gemm_breg.hip breg_ln_kernel): the consumer reads the producing Linear's
+  // output (bias included) and the residual, normalises the rows and its column-tile-0 workgroups
+  // store them as the next residual.  17 of the 19 LayerNorm launches of a token go away
+  // (CAPGEN_DECODE_LN_FOLD=0: separate launches).
   // Folded below 1024 rows (greedy's 256; CAPGEN_DECODE_LN_FOLD=2: at any row count): at beam-5's
   // 1280 rows the separate launches measured faster (12.83-12.84 vs 12.88-12.92 ms per batch with
   // only the cross-query site folded, 13.77-13.80 with all three), where greedy gains 3.5 %.
@@ -1853,24 +1853,16 @@ struct capgen_engine {
   }
   // one decode Linear: C (+)= X . W^T (+ bias) (ReLU); lng: the A rows are LayerNorm inputs, normalised
   // with (lng, lnb) and the row mask rm inside the GEMM, the normalised rows stored into lny
-  void dec_linear(const void* X, int64_t woff, int M, int N, int K, void* C, const float* bias, int relu, int beta,
-                  hipStream_t s, const float* lng = nullptr, const float* lnb = nullptr, void* lny = nullptr,
-                  const RowMask* rm = nullptr) {
+  void dec_linear(const void* X, int64_t woff, int M, int N, int K, void* C, const float* bias, int relu,
+                  hipStream_t s, const void* lnres = nullptr, const float* lng = nullptr, const float* lnb = nullptr,
+                  void* lny = nullptr, const RowMask* rm = nullptr) {
     GemmArgs ga;
     ga.M = M, ga.N = N, ga.K = K, ga.A = X, ga.lda = K, ga.B = W(woff), ga.ldb = K, ga.C = C, ga.ldc = N;
-    ga.bt = DT(woff), ga.bias = bias, ga.relu = relu, ga.beta = beta, ga.prio = prio(s);
-    ga.ln_gamma = lng, ga.ln_beta = lnb, ga.ln_y = lny;
+    ga.bt = DT(woff), ga.bias = bias, ga.relu = relu, ga.prio = prio(s);
+    ga.ln_res = lnres, ga.ln_gamma = lng, ga.ln_beta = lnb, ga.ln_y = lny;
     if (rm) ga.ln_ids = rm->ids, ga.ln_ids_ld = rm->ids_ld, ga.ln_pad = rm->pad_idx;
     if (stamp_on) ga.stamp = stamp(s, std::string(lng ? "gemm fwd+ln " : "gemm fwd ") + dims(M, N, K));
     gemm(ga, act, act, false, false, s);
-  }
-
-  // y = LN(v) (* row mask) as its own launch, v already holding bias and residual
-  void dec_ln(int M, const void* v, const float* gamma, const float* beta, const RowMask* rm, void* y, hipStream_t s) {
-    LnFwd l;
-    l.M = M, l.d = L.dd, l.a = v, l.gamma = gamma, l.beta = beta, l.y = y;
-    if (rm) l.mask = *rm;
-    lnf(l, s);
   }
 
   void dec_step(int R, int Bimg, int N, int t, void* cache, const int32_t* ids, bool want_attn, hipStream_t s,
@@ -1894,9 +1886,9 @@ struct capgen_engine {
         ga.M = R, ga.N = 3 * dd, ga.K = dd, ga.A = g.x, ga.lda = dd, ga.B = W(w.Wqkv), ga.ldb = dd;
         ga.C = g.q, ga.ldc = dd, ga.C2 = at(cl, (int64_t)t * 2 * dd), ga.ldc2 = cld, ga.nsplit = dd;
         ga.bt = DT(w.Wqkv);
-        if (fold && l > 0) {  // the previous block's FFN LayerNorm (v in g.x2) -> g.x
+        if (fold && l > 0) {  // the previous block's FFN LayerNorm (W2 output in tmp + x2) -> g.x
           const auto& wp = L.dec[l - 1];
-          ga.A = g.x2, ga.ln_gamma = P(wp.lfg), ga.ln_beta = P(wp.lfb), ga.ln_y = g.x;
+          ga.A = g.tmp, ga.ln_res = g.x2, ga.ln_gamma = P(wp.lfg), ga.ln_beta = P(wp.lfb), ga.ln_y = g.x;
           ga.ln_ids = rm.ids, ga.ln_ids_ld = rm.ids_ld, ga.ln_pad = rm.pad_idx;
         }
         ga.prio = prio(s);
@@ -1917,9 +1909,9 @@ struct capgen_engine {
       sg.kv_row = kv_row, sg.kv_row_ld = Tc;
       sg.temperature = std::sqrt((float)dkd);
       attf(sg, g.att, nullptr, act, s);
-      if (fold) {  // v = att . Wo_s^T + x into g.x; the cross-query GEMM normalises it (-> g.x1)
-        dec_linear(g.att, w.Wo_s, R, dd, dd, g.x, nullptr, 0, 1, s);
-        dec_linear(g.x, w.Wq_c, R, dd, dd, g.q, nullptr, 0, 0, s, P(w.lsg), P(w.lsb), g.x1);
+      if (fold) {  // att . Wo_s^T into tmp; the cross-query GEMM normalises tmp + x (-> g.x1)
+        dec_linear(g.att, w.Wo_s, R, dd, dd, g.tmp, nullptr, 0, s);
+        dec_linear(g.tmp, w.Wq_c, R, dd, dd, g.q, nullptr, 0, s, g.x, P(w.lsg), P(w.lsb), g.x1);
       } else {
         linear(g.att, dd, w.Wo_s, dd, g.tmp, dd, act, R, dd, dd, nullptr, 0, s, DT(w.Wo_s));
         LnFwd l1;
@@ -1948,13 +1940,17 @@ struct capgen_engine {
         c.o_ld = dd, c.o_bs = dd;
       }
       attf(c, g.att, want_p ? g.Pc : nullptr, act, s);
-      if (fold) {  // v = att . Wo_c^T + x1 into g.x1; the FFN's first GEMM normalises it (-> g.x2);
-                   // v = h . W2^T + b2 + x2 into g.x2, normalised by the next block's QKV GEMM
-        dec_linear(g.att, w.Wo_c, R, dd, dd, g.x1, nullptr, 0, 1, s);
-        dec_linear(g.x1, w.W1, R, L.fd, dd, g.h, P(w.b1), 1, 0, s, P(w.lcg), P(w.lcb), g.x2);
-        dec_linear(g.h, w.W2, R, dd, L.fd, g.x2, P(w.b2), 0, 1, s);
-        // the last block's FFN LayerNorm feeds the classifier: its own launch
-        if (l == L.Ld - 1) dec_ln(R, g.x2, P(w.lfg), P(w.lfb), &rm, g.x, s);
+      if (fold) {  // att . Wo_c^T into tmp, the FFN's first GEMM normalises tmp + x1 (-> g.x2);
+                   // h . W2^T + b2 into tmp, normalised with x2 by the next block's QKV GEMM
+        dec_linear(g.att, w.Wo_c, R, dd, dd, g.tmp, nullptr, 0, s);
+        dec_linear(g.tmp, w.W1, R, L.fd, dd, g.h, P(w.b1), 1, s, g.x1, P(w.lcg), P(w.lcb), g.x2);
+        dec_linear(g.h, w.W2, R, dd, L.fd, g.tmp, P(w.b2), 0, s);
+        if (l == L.Ld - 1) {  // the last block's FFN LayerNorm feeds the classifier: its own launch
+          LnFwd l3;
+          l3.M = R, l3.d = dd, l3.a = g.tmp, l3.res = g.x2, l3.gamma = P(w.lfg), l3.beta = P(w.lfb);
+          l3.mask = rm, l3.y = g.x;
+          lnf(l3, s);
+        }
         continue;
       }
       linear(g.att, dd, w.Wo_c, dd, g.tmp, dd, act, R, dd, dd, nullptr, 0, s, DT(w.Wo_c));
@@ -2474,9 +2470,10 @@ int capgen_debug_gemm_tiled(int M, int N, int K, const void* A, int64_t lda, con
   });
 }
 
-int capgen_debug_gemm_tiled_ln(int M, int N, const void* A, const void* B, void* Bt, void* Cp, int out_dtype,
-                               const float* bias, int beta, int relu, const float* ln_gamma, const float* ln_beta,
-                               void* ln_y, const int32_t* ln_ids, int64_t ln_ids_ld, int ln_pad, void* stream) {
+int capgen_debug_gemm_tiled_ln(int M, int N, const void* A, const void* ln_res, const void* B, void* Bt, void* Cp,
+                               int out_dtype, const float* bias, int beta, int relu, const float* ln_gamma,
+                               const float* ln_beta, void* ln_y, const int32_t* ln_ids, int64_t ln_ids_ld, int ln_pad,
+                               void* stream) {
   return guarded([&] {
     gemm_init();
     const hipStream_t s = (hipStream_t)stream;
@@ -2485,7 +2482,7 @@ int capgen_debug_gemm_tiled_ln(int M, int N, const void* A, const void* B, void*
     GemmArgs ga;
     ga.M = M, ga.N = N, ga.K = K, ga.A = A, ga.lda = K, ga.B = B, ga.ldb = K, ga.C = Cp, ga.ldc = N;
     ga.bias = bias, ga.beta = beta, ga.relu = relu, ga.bt = Bt;
-    ga.ln_gamma = ln_gamma, ga.ln_beta = ln_beta, ga.ln_y = ln_y;
+    ga.ln_res = ln_res, ga.ln_gamma = ln_gamma, ga.ln_beta = ln_beta, ga.ln_y = ln_y;
     ga.ln_ids = ln_ids, ga.ln_ids_ld = ln_ids_ld, ga.ln_pad = ln_pad;
     require(ln_gamma && gemm_breg_ok(ga), "debug_gemm_tiled_ln: a shape the folded-LayerNorm kernel does not take");
     gemm(ga, DType::BF16, dt(out_dtype), false, false, s);

@@ -54,10 +54,11 @@ struct GemmArgs {
   uint64_t* stamp = nullptr;  // diagnostic timestamps (capgen_common.h StampScope); grouped: p[0]'s
   int wt = -1;                // write-through (sc1) C stores (bf16 path): 1/0, -1 = wt_default()
   int pad3_ = 0;
-  // LayerNorm folded into the consumer (register-B path, K = 512; the decode step): A holds the
-  // LayerNorm INPUT rows v, the kernel multiplies y = ((v - mean) * rstd * ln_gamma + ln_beta) * keep
-  // (keep = 0 for rows m with ln_ids[m * ln_ids_ld] == ln_pad when ln_ids is set; modules.py:86-90,
-  // 114-120), and the workgroups of column tile 0 also store y into ln_y ([M][K] bf16, not A)
+  // LayerNorm folded into the consumer (register-B path, K = 512; the decode step): the LayerNorm
+  // input is v = A (+ ln_res, bf16 [M][K]), the kernel multiplies
+  // y = ((v - mean) * rstd * ln_gamma + ln_beta) * keep (keep = 0 for rows m with
+  // ln_ids[m * ln_ids_ld] == ln_pad when ln_ids is set; modules.py:86-90, 114-120), and the workgroups
+  // of column tile 0 also store y into ln_y ([M][K] bf16; neither A nor ln_res)
   const float* ln_gamma = nullptr;
   const float* ln_beta = nullptr;
   void* ln_y = nullptr;
@@ -65,9 +66,10 @@ struct GemmArgs {
   int64_t ln_ids_ld = 0;
   int ln_pad = 0;
   int pad4_ = 0;
+  const void* ln_res = nullptr;
 };
-// 4 ints + 34 eight-byte fields (pointers, int64s, int/float pairs): the size leaves no room for padding
-static_assert(sizeof(GemmArgs) == 16 + 34 * 8, "GemmArgs must have no padding");
+// 4 ints + 35 eight-byte fields (pointers, int64s, int/float pairs): the size leaves no room for padding
+static_assert(sizeof(GemmArgs) == 16 + 35 * 8, "GemmArgs must have no padding");
 
 // Independent GEMMs of one layout launched as ONE grid (tiles problem after problem).
 constexpr int kMaxGroup = 8;

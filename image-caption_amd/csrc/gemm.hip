@@ -270,6 +270,7 @@ void gemm_hz_regions(const GemmArgs& g, DType in, DType out, bool ta, bool tb, s
   v.push_back(rd(g.ln_beta, g.K * 4));
   v.push_back(blk(g.ln_ids, g.ln_ids ? g.M : 0, 4, g.ln_ids_ld * 4, RD));
   v.push_back(wr(g.ln_y, (int64_t)g.M * g.K * 2));
+  v.push_back(rd(g.ln_res, (int64_t)g.M * g.K * 2));
 }
 
 static void gemm_impl(const GemmArgs& g, DType in, DType out, bool ta, bool tb, hipStream_t s);

@@ -132,11 +132,11 @@ __global__ void __launch_bounds__(256) breg_kernel(GemmArgs g) {
   tile_epilogue<TO, FM, FN, BM, WN>(g, acc, m0, n0, 0, w, lane, alpha, 0, 1);
 }
 
-// The LayerNorm of the decode step folded into its consumer (GemmArgs::ln_gamma; K = 512 = d): A holds
-// the LayerNorm INPUT rows v (the producing GEMM's epilogue already added bias and residual into the
-// residual buffer, beta = 1), so a 32-row tile's whole A block (32 KB) is loaded once, normalised in
-// registers and left in LDS for all 16 k-steps -- the separate LayerNorm launch and its dependent
-// boundary go away.  Half-wave h of wave w owns rows 2 w + h + 8 i (i < 4); its lane c holds columns
+// The LayerNorm of the decode step folded into its consumer (GemmArgs::ln_gamma; K = 512 = d): the
+// LayerNorm input is v = A + ln_res (the producing Linear's output, bias included, and the residual),
+// so a 32-row tile's whole A block (32 KB) is loaded once with its residual, normalised in registers
+// and left in LDS for all 16 k-steps -- the separate LayerNorm launch and its dependent boundary go
+// away.  Half-wave h of wave w owns rows 2 w + h + 8 i (i < 4); its lane c holds columns
 // 16 c .. 16 c + 15 of each, so the row statistics are 5 xor-shuffles.  The workgroups of column tile
 // 0 also store y (the next producer's residual).  B as in breg_kernel: 16 k-steps in two register
 // batches of 8, both issued before the A block.
@@ -167,14 +167,21 @@ __global__ void __launch_bounds__(256) breg_ln_kernel(GemmArgs g) {
     for (int q = 0; q < QB; ++q) bq[b][q] = *reinterpret_cast<const bf16x8*>(brow + (int64_t)(b * QB + q) * 512);
 
   const int h = lane >> 5, c = lane & 31;
-  u32x4 av[4][2];
+  // (an absent residual reads the A rows again and adds nothing: resw = 0)
+  const bf16* __restrict__ Rs = g.ln_res ? reinterpret_cast<const bf16*>(g.ln_res) : A;
+  const int64_t ldr = g.ln_res ? KD : g.lda;
+  const float resw = g.ln_res ? 1.f : 0.f;
+  u32x4 av[4][2], rv[4][2];
   int idv[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = min(m0 + 2 * w + h + 8 * i, M - 1);
     const bf16* p = A + (int64_t)m * g.lda + 16 * c;
+    const bf16* q = Rs + (int64_t)m * ldr + 16 * c;
     av[i][0] = *reinterpret_cast<const u32x4*>(p);
     av[i][1] = *reinterpret_cast<const u32x4*>(p + 8);
+    rv[i][0] = *reinterpret_cast<const u32x4*>(q);
+    rv[i][1] = *reinterpret_cast<const u32x4*>(q + 8);
     idv[i] = g.ln_ids ? g.ln_ids[(int64_t)m * g.ln_ids_ld] : 0;
   }
   float gm[16], bt[16];
@@ -192,8 +199,9 @@ __global__ void __launch_bounds__(256) breg_ln_kernel(GemmArgs g) {
     float x[16];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      x[2 * e] = __uint_as_float(av[i][e >> 2][e & 3] << 16);
-      x[2 * e + 1] = __uint_as_float(av[i][e >> 2][e & 3] & 0xffff0000u);
+      x[2 * e] = fmaf(resw, __uint_as_float(rv[i][e >> 2][e & 3] << 16), __uint_as_float(av[i][e >> 2][e & 3] << 16));
+      x[2 * e + 1] = fmaf(resw, __uint_as_float(rv[i][e >> 2][e & 3] & 0xffff0000u),
+                          __uint_as_float(av[i][e >> 2][e & 3] & 0xffff0000u));
     }
     float s = 0.f;
 #pragma unroll
@@ -282,7 +290,8 @@ static bool breg_wide(const GemmArgs& g) { return g.N >= 1536 && g.M >= 1024; }
 
 bool gemm_breg_ok(const GemmArgs& g) {
   const int kq = breg_wide(g) ? 128 : 256;  // 32 * QB
-  const bool ln_ok = !g.ln_gamma || (g.K == 512 && g.ln_beta && g.ln_y && g.ln_y != g.A &&
+  const bool ln_ok = !g.ln_gamma || (g.K == 512 && g.ln_beta && g.ln_y && g.ln_y != g.A && g.ln_y != g.ln_res &&
+                                     ((uintptr_t)g.ln_res & 15) == 0 &&
                                      ((uintptr_t)g.ln_y & 15) == 0 && ((uintptr_t)g.ln_gamma & 15) == 0 &&
                                      ((uintptr_t)g.ln_beta & 15) == 0);
   return g.bt && g.M >= 1 && g.N % 64 == 0 && g.K >= kq && g.K % kq == 0 && g.lda % 8 == 0 &&

@@ -159,12 +159,14 @@ int capgen_debug_gemm_tiled(int M, int N, int K, const void* A, int64_t lda, con
                             const void* aux, int64_t ldaux, void* stream);
 
 /* Kernel test hook for the register-B GEMM with the decode step's folded LayerNorm (K = 512): as
- * capgen_debug_gemm_tiled (tb = 0) with A holding LayerNorm inputs v; the kernel multiplies
- * y = ((v - mean) * rstd * ln_gamma + ln_beta) * keep (eps 1e-6; keep = 0 for rows m with
- * ln_ids[m * ln_ids_ld] == ln_pad when ln_ids is non-null) and also stores y into ln_y ([M][512] bf16). */
-int capgen_debug_gemm_tiled_ln(int M, int N, const void* A, const void* B, void* Bt, void* C, int out_dtype,
-                               const float* bias, int beta, int relu, const float* ln_gamma, const float* ln_beta,
-                               void* ln_y, const int32_t* ln_ids, int64_t ln_ids_ld, int ln_pad, void* stream);
+ * capgen_debug_gemm_tiled (tb = 0) with LayerNorm inputs v = A (+ ln_res if non-null; both [M][512]
+ * bf16); the kernel multiplies y = ((v - mean) * rstd * ln_gamma + ln_beta) * keep (eps 1e-6; keep = 0
+ * for rows m with ln_ids[m * ln_ids_ld] == ln_pad when ln_ids is non-null) and also stores y into ln_y
+ * ([M][512] bf16). */
+int capgen_debug_gemm_tiled_ln(int M, int N, const void* A, const void* ln_res, const void* B, void* Bt, void* C,
+                               int out_dtype, const float* bias, int beta, int relu, const float* ln_gamma,
+                               const float* ln_beta, void* ln_y, const int32_t* ln_ids, int64_t ln_ids_ld, int ln_pad,
+                               void* stream);
 
 /* Experiment hook: force a GEMM tile/wave/pipeline variant (0 = production heuristic). */
 int capgen_debug_gemm_variant(int variant);

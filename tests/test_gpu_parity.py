@@ -804,8 +804,9 @@ def test_breg_decode_tracks_ring_decode(set_knob):
 @pytest.mark.parametrize("epi", ["plain", "bias_relu_mask", "beta_f32"])
 def test_gemm_folded_layernorm_vs_torch(M, N, epi):
     """The decode step's LayerNorm folded into the register-B GEMM (gemm_breg.hip breg_ln_kernel,
-    CAPGEN_DECODE_LN_FOLD): A holds LayerNorm inputs v; the kernel normalises them (modules.py:86-90,
-    eps 1e-6, gamma / beta, rows whose token is the pad id zeroed as modules.py:114-120) and multiplies.
+    CAPGEN_DECODE_LN_FOLD): the LayerNorm input is v = A + the residual (A alone in "plain"); the kernel
+    normalises it (modules.py:86-90, eps 1e-6, gamma / beta, rows whose token is the pad id zeroed as
+    modules.py:114-120) and multiplies.
     Against torch: the stored normalised rows y within one bf16 rounding of the f32 LayerNorm, and the
     product within the register-B test's bound computed on torch's LayerNorm of the same v; M tails."""
     import ctypes as C
@@ -813,14 +814,17 @@ def test_gemm_folded_layernorm_vs_torch(M, N, epi):
     lib = _lib.load()
     K = 512
     g = torch.Generator(device="cpu").manual_seed(M + 5 * N + len(epi))
-    v = (3.0 * torch.randn(M, K, generator=g) + 0.5).bfloat16()
+    a = (3.0 * torch.randn(M, K, generator=g) + 0.5).bfloat16()
+    with_res = epi != "plain"  # the producing Linear's output + the residual (the decode chain's form)
+    res = torch.randn(M, K, generator=g).bfloat16()
+    v = a.float() + res.float() if with_res else a.float()
     gamma, beta = 1.0 + 0.3 * torch.randn(K, generator=g), 0.2 * torch.randn(K, generator=g)
     Bm = torch.randn(N, K, generator=g).bfloat16()
     bias = torch.randn(N, generator=g)
     c0 = torch.randn(M, N, generator=g)
     ids = torch.randint(0, 4, (M,), generator=g, dtype=torch.int32)  # pad id 0: ~1/4 of the rows
     masked = epi == "bias_relu_mask"
-    y = torch.nn.functional.layer_norm(v.float(), (K,), gamma, beta, eps=1e-6)
+    y = torch.nn.functional.layer_norm(v, (K,), gamma, beta, eps=1e-6)
     if masked:
         y = y * (ids != 0).float()[:, None]
     ref = y.bfloat16().float() @ Bm.float().t()
@@ -832,8 +836,9 @@ def test_gemm_folded_layernorm_vs_torch(M, N, epi):
     Bt = torch.empty(N * K, dtype=torch.bfloat16, device=DEV)
     Cd = c0.to(DEV) if out_f32 else torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
     Yd = torch.full((M, K), float("nan"), dtype=torch.bfloat16, device=DEV)
-    vd, Bd, bd, gd, btd, idd = (t.to(DEV) for t in (v, Bm, bias, gamma, beta, ids))
-    _lib.check(lib.capgen_debug_gemm_tiled_ln(M, N, C.c_void_p(vd.data_ptr()), C.c_void_p(Bd.data_ptr()),
+    ad, rd, Bd, bd, gd, btd, idd = (t.to(DEV) for t in (a, res, Bm, bias, gamma, beta, ids))
+    _lib.check(lib.capgen_debug_gemm_tiled_ln(M, N, C.c_void_p(ad.data_ptr()),
+                                              C.c_void_p(rd.data_ptr()) if with_res else None, C.c_void_p(Bd.data_ptr()),
                                               C.c_void_p(Bt.data_ptr()), C.c_void_p(Cd.data_ptr()),
                                               0 if out_f32 else 1, C.c_void_p(bd.data_ptr()) if masked else None,
                                               1 if out_f32 else 0, 1 if masked else 0, C.c_void_p(gd.data_ptr()),
