@@ -210,7 +210,11 @@ struct capgen_engine {
   // re-tile the fronts' weights that overlap the arena range [off, off + n) from the shadow (a matrix
   // cut by a range boundary is re-tiled by both ranges' calls; the later one, on the same stream, sees
   // the whole matrix updated)
+  // the weight version: bumped at every enqueued change of the bf16 shadow (each one is followed by
+  // retile), so the decode tiles are rebuilt only when the weights moved
+  uint64_t wver = 1, dtiles_ver = 0;
   void retile(int64_t off, int64_t n, hipStream_t s, bool trans_only = false) {
+    ++wver;
     for (auto& kv : tiled)
       if (kv.first < off + n && kv.first + (int64_t)std::abs(kv.second.second) * 512 > off) {
         if (kv.second.second < 0) qkv_tile_weights_t(shadow + kv.first, 512, wtile + kv.second.first, s);
@@ -248,6 +252,13 @@ struct capgen_engine {
   }
   void build_dtiles(hipStream_t s) {
     if (!dtiles) return;
+    // skipped while the tiles match the weights (~0.12 ms per greedy / beam call); a build captured
+    // into a graph runs at every replay
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    CAPGEN_HIP(hipStreamIsCapturing(s, &cs));
+    const bool capturing = cs != hipStreamCaptureStatusNone;
+    if (!capturing && dtiles_ver == wver) return;
+    if (!capturing) dtiles_ver = wver;
     for (const auto& t : dtile_list()) {
       auto it = dtile.find(t[0]);
       if (it != dtile.end()) gemm_tile_b(shadow + t[0], t[2], 0, (int)t[1], (int)t[2], dtiles + it->second, s);

@@ -773,6 +773,32 @@ def test_gemm_register_b_vs_torch(M, N, K, tb, epi):
     assert err <= tol, (err, tol)
 
 
+def test_decode_tiles_follow_weight_updates():
+    """The decode step's weight fragment pieces are rebuilt only when the weights moved (engine.hip
+    build_dtiles, weight version bumped by every shadow update): decoding, then loading other weights
+    (and then one bf16 train step), must decode exactly as a fresh engine holding those weights."""
+    from capgen.engine import Engine
+    _, cfg, sd, e, f, p, c = _c2_setup(B=64, dtype="bf16", weights="fixture")
+    fd, pd, cd = f.to(DEV).bfloat16(), p.to(DEV), c.to(DEV)
+    e.set_training(False)
+    e.greedy(fd, pd)
+    sd2 = {k: v * 0.9 if v.ndim == 2 else v for k, v in sd.items()}
+    e.load_state_dict(sd2)
+    fresh = Engine(cfg.replace(dtype="bf16"), DEV)
+    fresh.load_state_dict(sd2)
+    fresh.set_training(False)
+    i_e, _ = e.greedy(fd, pd)
+    i_f, _ = fresh.greedy(fd, pd)
+    assert torch.equal(i_e, i_f)
+    e.train_step(fd, pd, cd)  # Adam moves e's weights (f32 atomics: copy them, do not re-train)
+    torch.cuda.synchronize()
+    fresh.set_params_arena(e.params_arena())
+    i_e, _ = e.greedy(fd, pd)
+    i_f, _ = fresh.greedy(fd, pd)
+    assert torch.equal(i_e, i_f)
+    assert torch.equal(e.beam(fd, pd, 5), fresh.beam(fd, pd, 5))
+
+
 def test_breg_decode_tracks_ring_decode(set_knob):
     """bf16 C4-style decode with the decoder Linears on the register-B GEMM (CAPGEN_BREG_DECODE,
     default on) against the LDS-ring GEMM: the products differ only in summation order inside the
