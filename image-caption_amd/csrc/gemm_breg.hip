@@ -134,17 +134,17 @@ __global__ void __launch_bounds__(256) breg_kernel(GemmArgs g) {
 
 // The LayerNorm of the decode step folded into its consumer (GemmArgs::ln_gamma; K = 512 = d): the
 // LayerNorm input is v = A + ln_res (the producing Linear's output, bias included, and the residual),
-// so a 32-row tile's whole A block (32 KB) is loaded once with its residual, normalised in registers
+// so a BM-row tile's whole A block (BM KB) is loaded once with its residual, normalised in registers
 // and left in LDS for all 16 k-steps -- the separate LayerNorm launch and its dependent boundary go
-// away.  Half-wave h of wave w owns rows 2 w + h + 8 i (i < 4); its lane c holds columns
+// away.  Half-wave h of wave w owns rows 2 w + h + 8 i (i < BM / 8); its lane c holds columns
 // 16 c .. 16 c + 15 of each, so the row statistics are 5 xor-shuffles.  The workgroups of column tile
 // 0 also store y (the next producer's residual).  B as in breg_kernel: 16 k-steps in two register
 // batches of 8, both issued before the A block.
 constexpr float kLnEps = 1e-6f;  // modules.py:57,105 (ops.hip LN_EPS)
 
-template <typename TO>
+template <typename TO, int BM>
 __global__ void __launch_bounds__(256) breg_ln_kernel(GemmArgs g) {
-  constexpr int BM = 32, BN = 64, QB = 8, KD = 512, KS = KD / 32, RB = KD * 2;
+  constexpr int BN = 64, QB = 8, KD = 512, KS = KD / 32, RB = KD * 2, RH = BM / 8;  // RH rows per half-wave
   constexpr int FM = BM / 16, WN = BN / 4;  // one 16-column fragment per wave
   __shared__ __attribute__((aligned(16))) char sA[BM * RB];
   StampScope stamp_scope(g.stamp);
@@ -171,10 +171,10 @@ __global__ void __launch_bounds__(256) breg_ln_kernel(GemmArgs g) {
   const bf16* __restrict__ Rs = g.ln_res ? reinterpret_cast<const bf16*>(g.ln_res) : A;
   const int64_t ldr = g.ln_res ? KD : g.lda;
   const float resw = g.ln_res ? 1.f : 0.f;
-  u32x4 av[4][2], rv[4][2];
-  int idv[4];
+  u32x4 av[RH][2], rv[RH][2];
+  int idv[RH];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < RH; ++i) {
     const int m = min(m0 + 2 * w + h + 8 * i, M - 1);
     const bf16* p = A + (int64_t)m * g.lda + 16 * c;
     const bf16* q = Rs + (int64_t)m * ldr + 16 * c;
@@ -194,7 +194,7 @@ __global__ void __launch_bounds__(256) breg_ln_kernel(GemmArgs g) {
   }
   bf16* __restrict__ Y = reinterpret_cast<bf16*>(g.ln_y);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < RH; ++i) {
     const int r = 2 * w + h + 8 * i;
     float x[16];
 #pragma unroll
@@ -278,14 +278,19 @@ void launch(const GemmArgs& g, hipStream_t s) {
 
 template <typename TO>
 void launch_ln(const GemmArgs& g, hipStream_t s) {
-  const int T = ((g.M + 31) / 32) * (g.N / 64);
-  breg_ln_kernel<TO><<<((T + 7) / 8) * 8, 256, 0, s>>>(g);
+  // 16-row tiles (greedy 8.73-8.75 vs 9.30-9.39 ms per C4 batch with 32-row ones; beam 5 folded with
+  // 16-row tiles 13.56-13.57 vs 12.82-12.84 unfolded, so beam keeps the separate LayerNorms)
+  const int T = ((g.M + 15) / 16) * (g.N / 64);
+  breg_ln_kernel<TO, 16><<<((T + 7) / 8) * 8, 256, 0, s>>>(g);
 }
 
 }  // namespace
 
-// the launch choice (tools/breg_probe.hip, kernel durations): 64 x 64 tiles with 4-step batches for
-// wide outputs at >= 1024 rows, else 32 x 64 tiles, 128-deep k-tiles and 8-step batches
+// the launch choice: 64 x 64 tiles with 4-step batches for wide outputs at >= 1024 rows
+// (tools/breg_probe.hip, kernel durations), else 16 x 64 tiles, 128-deep k-tiles and 8-step batches --
+// twice the workgroups of the probe's 32 x 64 choice, each with half the serial latency: C4 greedy
+// 8.17-8.22 vs 8.61-8.70 ms, beam 5 12.64-12.70 vs 12.80-12.83 (in the decode, alternating libraries,
+// profiles/r05_decode_16row_tiles.txt; 16-row tiles for the wide outputs too: beam 13.24-13.29)
 static bool breg_wide(const GemmArgs& g) { return g.N >= 1536 && g.M >= 1024; }
 
 bool gemm_breg_ok(const GemmArgs& g) {
@@ -309,10 +314,10 @@ void gemm_breg(const GemmArgs& g, DType out, hipStream_t s) {
   const bool wide = breg_wide(g);
   if (out == DType::BF16) {
     if (wide) launch<bf16, 64, 64, 4, 2, 2>(g, s);
-    else launch<bf16, 32, 64, 8, 2, 4>(g, s);
+    else launch<bf16, 16, 64, 8, 2, 4>(g, s);
   } else {
     if (wide) launch<float, 64, 64, 4, 2, 2>(g, s);
-    else launch<float, 32, 64, 8, 2, 4>(g, s);
+    else launch<float, 16, 64, 8, 2, 4>(g, s);
   }
 }
 
