@@ -1851,16 +1851,17 @@ struct capgen_engine {
   // output (bias included) and the residual, normalises the rows and its column-tile-0 workgroups
   // store them as the next residual.  17 of the 19 LayerNorm launches of a token go away
   // (CAPGEN_DECODE_LN_FOLD=0: separate launches).
-  // Folded below 1024 rows (greedy's 256; CAPGEN_DECODE_LN_FOLD=2: at any row count): at beam-5's
-  // 1280 rows the separate launches measured faster (12.83-12.84 vs 12.88-12.92 ms per batch with
-  // only the cross-query site folded, 13.77-13.80 with all three), where greedy gains 3.5 %.
+  // Every site below 1024 rows (greedy's 256; CAPGEN_DECODE_LN_FOLD=2: at any row count); at beam-5's
+  // 1280 rows only the cross-query site: folding the QKV / FFN-up sites too replaces their 64 x 64
+  // register-B tiles and measured slower (13.56-13.57 vs 12.82-12.84 ms per batch).
   int decode_ln_fold = knob(Knob::DecodeLnFold);
-  bool ln_fold(int M) const {
-    if (!decode_ln_fold || !breg_decode() || L.dd != 512 || L.fd % 64 != 0) return false;
-    if (decode_ln_fold != 2 && M >= 1024) return false;
+  // 2: every site, 1: only the cross-query site (beam's rows: 12.50-12.53 vs 12.62-12.73 ms per C4
+  // batch with none, profiles/r05_decode_16row_tiles.txt), 0: none
+  int ln_fold(int M) const {
+    if (!decode_ln_fold || !breg_decode() || L.dd != 512 || L.fd % 64 != 0) return 0;
     for (const auto& w : L.dec)
-      if (!DT(w.Wqkv) || !DT(w.Wq_c) || !DT(w.W1)) return false;
-    return true;
+      if (!DT(w.Wqkv) || !DT(w.Wq_c) || !DT(w.W1)) return 0;
+    return decode_ln_fold == 2 || M < 1024 ? 2 : 1;
   }
   // one decode Linear: C (+)= X . W^T (+ bias) (ReLU); lng: the A rows are LayerNorm inputs, normalised
   // with (lng, lnb) and the row mask rm inside the GEMM, the normalised rows stored into lny
@@ -1888,7 +1889,8 @@ struct capgen_engine {
     RowMask rm{};
     rm.ids = ids + t, rm.ids_ld = Tc, rm.pad_idx = cfg.pad_idx;
     const int64_t kvld = (int64_t)L.Ld * 2 * dd, cld = (int64_t)Tc * 2 * dd;
-    const bool fold = ln_fold(R);
+    const int fmode = ln_fold(R);
+    const bool fold = fmode == 2, fold1 = fmode >= 1;  // every site / the cross-query site
     for (int l = 0; l < L.Ld; ++l) {
       const auto& w = L.dec[l];
       void* cl = at(cache, (int64_t)l * R * cld);
@@ -1920,7 +1922,7 @@ struct capgen_engine {
       sg.kv_row = kv_row, sg.kv_row_ld = Tc;
       sg.temperature = std::sqrt((float)dkd);
       attf(sg, g.att, nullptr, act, s);
-      if (fold) {  // att . Wo_s^T into tmp; the cross-query GEMM normalises tmp + x (-> g.x1)
+      if (fold1) {  // att . Wo_s^T into tmp; the cross-query GEMM normalises tmp + x (-> g.x1)
         dec_linear(g.att, w.Wo_s, R, dd, dd, g.tmp, nullptr, 0, s);
         dec_linear(g.tmp, w.Wq_c, R, dd, dd, g.q, nullptr, 0, s, g.x, P(w.lsg), P(w.lsb), g.x1);
       } else {

@@ -889,7 +889,7 @@ def test_decode_layernorm_fold_tracks_separate_launches(set_knob, fold):
     >= 90 % of the images and with the fp32 engine's no worse than 5 points below the unfolded engine's."""
     set_knob("DECODE_LN_FOLD", 0)
     _, cfg, sd, e0, f, p, c = _c2_setup(B=256, dtype="bf16", weights="fixture")
-    set_knob("DECODE_LN_FOLD", fold)  # 1: folded below 1024 rows (greedy, not beam-5), 2: at any row count
+    set_knob("DECODE_LN_FOLD", fold)  # 1: every site at greedy rows, the cross-query site at beam-5 rows; 2: every site
     _, _, _, e1, _, _, _ = _c2_setup(B=256, dtype="bf16", weights="fixture")
     _, _, _, e32, _, _, _ = _c2_setup(B=256, dtype="fp32", weights="fixture")
     fd, pd = f.to(DEV), p.to(DEV)
