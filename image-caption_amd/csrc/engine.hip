@@ -243,8 +243,12 @@ struct capgen_engine {
     auto it = dtile.find(off);
     return it == dtile.end() || !dtiles ? nullptr : dtiles + it->second;
   }
+  bf16* emb_bf = nullptr;  // bf16 decode: the word-embedding table, read by the Wel GEMM through the ids
   void ensure_dtiles() {  // (outside any capture)
     if (dtiles || !breg_decode()) return;
+#ifndef CAPGEN_NO_GATHER_FOLD
+    if (L.dwe % 8 == 0) CAPGEN_HIP(hipMalloc(&emb_bf, (size_t)L.V * L.dwe * 2));
+#endif
     int64_t tot = 0;
     for (const auto& t : dtile_list())
       if (t[1] % 16 == 0 && t[2] % 32 == 0) dtile[t[0]] = tot, tot += t[1] * t[2];
@@ -259,6 +263,7 @@ struct capgen_engine {
     const bool capturing = cs != hipStreamCaptureStatusNone;
     if (!capturing && dtiles_ver == wver) return;
     if (!capturing) dtiles_ver = wver;
+    if (emb_bf) to_bf16(P(L.emb), emb_bf, (size_t)L.V * L.dwe, s);
     for (const auto& t : dtile_list()) {
       auto it = dtile.find(t[0]);
       if (it != dtile.end()) gemm_tile_b(shadow + t[0], t[2], 0, (int)t[1], (int)t[2], dtiles + it->second, s);
@@ -1182,6 +1187,7 @@ struct capgen_engine {
 
   // Adam over arena ranges; ranges are 64-element aligned so the bf16 shadow slices line up
   void adam_range(int64_t off, int64_t n, hipStream_t s, int grid_cap = 0) {
+    ++wver;  // (the embedding table has no shadow: its bf16 decode copy follows the version too)
     const int64_t ns = shadow ? std::max<int64_t>(0, std::min(n, L.n_dense - off)) : 0;
     // the fronts' tiled weights in this range: written by the Adam kernel itself (else re-tiled after)
     AdamTiles at;
@@ -1227,6 +1233,7 @@ struct capgen_engine {
   }
   // the bucket's all-reduce (DP) + Adam on the bucket stream (its producers already waited for)
   void bucket_update(int64_t off, int64_t n, int grid_cap = 0) {
+    ++wver;
     zbuckets.push_back({off, n});
     const int zw = zworld();
     if (zsharded() && n % (4 * zw) == 0) {  // sharded update (ZeRO-1); buckets are 64-element aligned
@@ -1525,6 +1532,7 @@ struct capgen_engine {
   }
 
   void adam(hipStream_t s) {
+    ++wver;
     adam_prepare(step, cfg.lr, cfg.beta1, cfg.beta2, adam_scal, s);
     adam_update(params, grads, am, av, (size_t)L.total, cfg.beta1, cfg.beta2, cfg.eps, adam_scal, shadow,
                 shadow ? (size_t)L.n_dense : 0, s);
@@ -1880,8 +1888,17 @@ struct capgen_engine {
   void dec_step(int R, int Bimg, int N, int t, void* cache, const int32_t* ids, bool want_attn, hipStream_t s,
                 const int32_t* kv_row = nullptr) {
     const int dd = L.dd, Hd = L.Hd, dkd = dd / Hd, Tc = L.maxlen;
-    embedding_gather(P(L.emb), ids + t, Tc, R, L.dwe, g.E, act, s, L.V);
-    linear(g.E, L.dwe, L.Wel, L.dwe, g.tmp, dd, act, R, dd, L.dwe, nullptr, 0, s, DT(L.Wel));
+    if (emb_bf && DT(L.Wel)) {  // the embedding rows gathered by the projection GEMM itself
+      GemmArgs ga;
+      ga.M = R, ga.N = dd, ga.K = L.dwe, ga.A = emb_bf, ga.lda = L.dwe, ga.B = W(L.Wel), ga.ldb = L.dwe;
+      ga.C = g.tmp, ga.ldc = dd, ga.bt = DT(L.Wel), ga.prio = prio(s);
+      ga.a_ids = ids + t, ga.a_ids_ld = Tc, ga.a_table_rows = L.V;
+      if (stamp_on) ga.stamp = stamp(s, "gemm fwd (gathered A) " + dims(R, dd, L.dwe));
+      gemm(ga, act, act, false, false, s);
+    } else {
+      embedding_gather(P(L.emb), ids + t, Tc, R, L.dwe, g.E, act, s, L.V);
+      linear(g.E, L.dwe, L.Wel, L.dwe, g.tmp, dd, act, R, dd, L.dwe, nullptr, 0, s, DT(L.Wel));
+    }
     LnFwd ln;
     ln.M = R, ln.d = dd, ln.a = g.tmp, ln.pe = pe + (int64_t)t * dd, ln.pe_L = 1, ln.gamma = P(L.dec_lng);
     ln.beta = P(L.dec_lnb), ln.y = g.x;
@@ -2093,7 +2110,7 @@ struct capgen_engine {
     if (es) (void)hipStreamSynchronize(es);
     drop_graph();
     if (comm) ncclCommDestroy(comm);
-    for (void* p : {(void*)params, (void*)grads, (void*)am, (void*)av, (void*)shadow, (void*)wtile, (void*)dtiles, (void*)pe, (void*)step,
+    for (void* p : {(void*)params, (void*)grads, (void*)am, (void*)av, (void*)shadow, (void*)wtile, (void*)dtiles, (void*)emb_bf, (void*)pe, (void*)step,
                     (void*)adam_scal, (void*)seed, (void*)scalars, (void*)gstripe, ws, gws, (void*)stamp_ring})
       if (p) (void)hipFree(p);
     if (count_host) (void)hipHostFree(count_host);

@@ -65,11 +65,15 @@ struct GemmArgs {
   const int32_t* ln_ids = nullptr;
   int64_t ln_ids_ld = 0;
   int ln_pad = 0;
-  int pad4_ = 0;
+  int a_table_rows = 0;  // a_ids: rows of the table A (hazard checker)
   const void* ln_res = nullptr;
+  // register-B path: A rows gathered by index -- row m of the product is A[a_ids[m * a_ids_ld]] (the
+  // decode step's word-embedding projection reads the bf16 embedding table directly)
+  const int32_t* a_ids = nullptr;
+  int64_t a_ids_ld = 0;
 };
-// 4 ints + 35 eight-byte fields (pointers, int64s, int/float pairs): the size leaves no room for padding
-static_assert(sizeof(GemmArgs) == 16 + 35 * 8, "GemmArgs must have no padding");
+// 4 ints + 37 eight-byte fields (pointers, int64s, int/float pairs): the size leaves no room for padding
+static_assert(sizeof(GemmArgs) == 16 + 37 * 8, "GemmArgs must have no padding");
 
 // Independent GEMMs of one layout launched as ONE grid (tiles problem after problem).
 constexpr int kMaxGroup = 8;

@@ -252,7 +252,9 @@ void gemm_hz_regions(const GemmArgs& g, DType in, DType out, bool ta, bool tb, s
   using namespace hz;
   const int64_t ei = dsize(in), eo = dsize(out);
   const int ncol = g.C2 ? g.nsplit : g.N;
-  v.push_back(ta ? blk(g.A, g.K, g.M * ei, g.lda * ei, RD) : blk(g.A, g.M, g.K * ei, g.lda * ei, RD));
+  v.push_back(g.a_ids ? blk(g.A, g.a_table_rows, g.K * ei, g.lda * ei, RD)
+                      : ta ? blk(g.A, g.K, g.M * ei, g.lda * ei, RD) : blk(g.A, g.M, g.K * ei, g.lda * ei, RD));
+  v.push_back(blk(g.a_ids, g.a_ids ? g.M : 0, 4, g.a_ids_ld * 4, RD));
   v.push_back(tb ? blk(g.B, g.K, g.N * ei, g.ldb * ei, RD) : blk(g.B, g.N, g.K * ei, g.ldb * ei, RD));
   v.push_back(blk(g.C, g.M, ncol * eo, g.ldc * eo, WR));
   if (g.beta) v.push_back(blk(g.C, g.M, ncol * eo, g.ldc * eo, RD));
@@ -300,6 +302,8 @@ static void gemm_impl(const GemmArgs& g, DType in, DType out, bool ta, bool tb, 
   require(!g.colsum || !g.beta, "gemm: colsum requires beta == 0");
   require(!g.bt || (in == DType::BF16 && !ta), "gemm: a tiled B (bt) needs the bf16 path with A stored [M][K]");
   require(!g.dec_stats || in == DType::BF16, "gemm: dec_stats is a bf16-path epilogue output");
+  require(!g.a_ids || (in == DType::BF16 && !ta && !tb && g.bt && gemm_breg_ok(g) && g.a_table_rows > 0),
+          "gemm: gathered A rows (a_ids) need the register-B path");
   require(!g.ln_gamma || (in == DType::BF16 && !ta && !tb && g.bt && gemm_breg_ok(g)),
           "gemm: a folded LayerNorm (ln_gamma) needs the register-B path (bf16, bt, K = 512)");
   require(!g.C2 || (in == DType::BF16 && g.nsplit % 4 == 0 && !g.beta && !g.colsum),

@@ -67,7 +67,8 @@ __global__ void __launch_bounds__(256) breg_kernel(GemmArgs g) {
 #pragma unroll
   for (int c = 0; c < CPT; ++c) {
     const int id = tid + 256 * c, row = id / (KT * 4), ch = id % (KT * 4);
-    arow[c] = A + (int64_t)min(m0 + row, M - 1) * g.lda + ch * 8;
+    const int m = min(m0 + row, M - 1);
+    arow[c] = A + (int64_t)(g.a_ids ? g.a_ids[(int64_t)m * g.a_ids_ld] : m) * g.lda + ch * 8;
     aoff[c] = row * RB + ((ch ^ (row & 7)) * 16);
   }
   u32x4 ar[AD][CPT];  // A(t) in ar[t % AD], loaded AD - 1 k-tiles before its LDS write
@@ -301,7 +302,7 @@ bool gemm_breg_ok(const GemmArgs& g) {
                                      ((uintptr_t)g.ln_beta & 15) == 0);
   return g.bt && g.M >= 1 && g.N % 64 == 0 && g.K >= kq && g.K % kq == 0 && g.lda % 8 == 0 &&
          ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.bt & 15) == 0 && !g.ce_stats && !g.dec_stats && !g.colsum &&
-         ln_ok;
+         ln_ok && !(g.a_ids && g.ln_gamma);
 }
 
 void gemm_breg(const GemmArgs& g, DType out, hipStream_t s) {
