@@ -1888,13 +1888,13 @@ struct capgen_engine {
   void dec_step(int R, int Bimg, int N, int t, void* cache, const int32_t* ids, bool want_attn, hipStream_t s,
                 const int32_t* kv_row = nullptr) {
     const int dd = L.dd, Hd = L.Hd, dkd = dd / Hd, Tc = L.maxlen;
-    if (emb_bf && DT(L.Wel)) {  // the embedding rows gathered by the projection GEMM itself
-      GemmArgs ga;
-      ga.M = R, ga.N = dd, ga.K = L.dwe, ga.A = emb_bf, ga.lda = L.dwe, ga.B = W(L.Wel), ga.ldb = L.dwe;
-      ga.C = g.tmp, ga.ldc = dd, ga.bt = DT(L.Wel), ga.prio = prio(s);
-      ga.a_ids = ids + t, ga.a_ids_ld = Tc, ga.a_table_rows = L.V;
-      if (stamp_on) ga.stamp = stamp(s, "gemm fwd (gathered A) " + dims(R, dd, L.dwe));
-      gemm(ga, act, act, false, false, s);
+    GemmArgs ge;  // the embedding rows gathered by the projection GEMM itself (where it takes the shape)
+    ge.M = R, ge.N = dd, ge.K = L.dwe, ge.A = emb_bf, ge.lda = L.dwe, ge.B = W(L.Wel), ge.ldb = L.dwe;
+    ge.C = g.tmp, ge.ldc = dd, ge.bt = DT(L.Wel), ge.prio = prio(s);
+    ge.a_ids = ids + t, ge.a_ids_ld = Tc, ge.a_table_rows = L.V;
+    if (emb_bf && ge.bt && gemm_breg_ok(ge)) {
+      if (stamp_on) ge.stamp = stamp(s, "gemm fwd (gathered A) " + dims(R, dd, L.dwe));
+      gemm(ge, act, act, false, false, s);
     } else {
       embedding_gather(P(L.emb), ids + t, Tc, R, L.dwe, g.E, act, s, L.V);
       linear(g.E, L.dwe, L.Wel, L.dwe, g.tmp, dd, act, R, dd, L.dwe, nullptr, 0, s, DT(L.Wel));
