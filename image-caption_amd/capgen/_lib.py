@@ -96,6 +96,7 @@ _SIGS = {
     "capgen_dp_set_global_count": (C.c_int, [_P, C.c_float]),
     "capgen_dp_sync_adam_state": (C.c_int, [_P]),
     "capgen_dp_comm_info": (C.c_int, [_P, _P, _P]),
+    "capgen_dp_check": (C.c_int, [_P, _P, _P]),
     "capgen_params_checksum": (C.c_int, [_P, _P]),
     "capgen_dp_buckets": (C.c_int, [_P, _P, _P, C.c_int, _P]),
     "capgen_dp_debug_shard": (C.c_int, [_P, C.c_int, C.c_int]),

@@ -282,6 +282,13 @@ class Engine:
         _lib.check(self.lib.capgen_dp_comm_info(self.h, C.byref(n), C.byref(r)))
         return n.value, r.value
 
+    def dp_check(self, loss: torch.Tensor | None = None):
+        """Run the data-parallel consistency check now (collective over the engine communicator, any
+        world size): every rank's global non-pad count and loss must agree (max == min); raises
+        RuntimeError otherwise.  `loss`: the [1] f32 device tensor the last step wrote (None = the
+        engine's internal loss).  The step runs the same check once by itself at world > 1."""
+        _lib.check(self.lib.capgen_dp_check(self.h, _ptr(loss), _stream(self.device)))
+
     def params_checksum(self) -> int:
         """Exact, order-independent checksum of the f32 parameters (equal on every rank of a DP run)."""
         v = C.c_uint64(0)

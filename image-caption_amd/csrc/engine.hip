@@ -244,15 +244,18 @@ struct capgen_engine {
     return it == dtile.end() || !dtiles ? nullptr : dtiles + it->second;
   }
   bf16* emb_bf = nullptr;  // bf16 decode: the word-embedding table, read by the Wel GEMM through the ids
+  bool dtiles_init = false;  // set once: a model whose Linears fit no tile shape allocates nothing, once
   void ensure_dtiles() {  // (outside any capture)
-    if (dtiles || !breg_decode()) return;
-#ifndef CAPGEN_NO_GATHER_FOLD
-    if (L.dwe % 8 == 0) CAPGEN_HIP(hipMalloc(&emb_bf, (size_t)L.V * L.dwe * 2));
-#endif
+    if (dtiles_init || !breg_decode()) return;
+    dtiles_init = true;
     int64_t tot = 0;
     for (const auto& t : dtile_list())
       if (t[1] % 16 == 0 && t[2] % 32 == 0) dtile[t[0]] = tot, tot += t[1] * t[2];
     if (tot) CAPGEN_HIP(hipMalloc(&dtiles, (size_t)tot * 2));
+#ifndef CAPGEN_NO_GATHER_FOLD
+    // only the tiled word-embedding projection reads the bf16 table
+    if (L.dwe % 8 == 0 && dtile.count(L.Wel)) CAPGEN_HIP(hipMalloc(&emb_bf, (size_t)L.V * L.dwe * 2));
+#endif
   }
   void build_dtiles(hipStream_t s) {
     if (!dtiles) return;
@@ -1017,6 +1020,7 @@ struct capgen_engine {
       cross_entropy_rows(a.logits, a.tgt, Md, L.V, cfg.pad_idx, a.loss_row, a.dlogits, act, s);
     }
     float* lo = loss_out ? loss_out : a.loss;
+    last_loss = lo;
     if (comm) {
       // data parallel: the mean CE over the GLOBAL batch (model.py:76) is the sum of the ranks'
       // partial sums / global count -- one 4-byte all-reduce, then the (Focal) loss and the
@@ -1560,15 +1564,21 @@ struct capgen_engine {
   // (the count all-reduce inside the forward -- captured in its graph -- gives the reference's mean over
   // the global batch, model.py:76) and so the same loss.  Max and min over the ranks of both, one
   // grouped 4-value exchange; a mismatch fails the step (non-zero status, capgen_last_error).
+  // `force` runs it regardless of world size and of an earlier check (capgen_dp_check: the world-1
+  // rehearsal of the exchange; the step's own call passes false).  `loss` null = the loss buffer the
+  // last forward wrote (its loss_out, or the internal one).
   bool dp_checked = false;
   float* dp_chk = nullptr;  // [4] device scratch: count max, count min, loss max, loss min
-  void dp_check(hipStream_t cs, const float* loss) {
-    if (dp_checked || !comm || world <= 1) return;
+  const float* last_loss = nullptr;
+  void dp_check(hipStream_t cs, const float* loss, bool force = false) {
+    if (!comm || (!force && (dp_checked || world <= 1))) return;
     dp_checked = true;
     if (!dp_chk) CAPGEN_HIP(hipMalloc(&dp_chk, 4 * sizeof(float)));
+    const float* lo = loss ? loss : last_loss;
+    require(a.count && lo, "dp_check: no train step yet");
     for (int i = 0; i < 2; ++i) {
       CAPGEN_HIP(hipMemcpyAsync(dp_chk + i, a.count, sizeof(float), hipMemcpyDeviceToDevice, cs));
-      CAPGEN_HIP(hipMemcpyAsync(dp_chk + 2 + i, loss ? loss : a.count, sizeof(float), hipMemcpyDeviceToDevice, cs));
+      CAPGEN_HIP(hipMemcpyAsync(dp_chk + 2 + i, lo, sizeof(float), hipMemcpyDeviceToDevice, cs));
     }
     NCCL_CHECK(ncclGroupStart());
     NCCL_CHECK(ncclAllReduce(dp_chk, dp_chk, 1, ncclFloat, ncclMax, comm, cs));
@@ -1711,6 +1721,9 @@ struct capgen_engine {
         CAPGEN_HIP(hipGraphDestroy(graph));
         gkey = k;
       }
+      // the replay runs the captured Adam and re-cast of the shadow with no host code: the weight
+      // version must move with it, or the decode tiles (build_dtiles) would keep the old weights
+      ++wver;
       CAPGEN_HIP(hipGraphLaunch(gexec, es));
     }
     leave(cs);
@@ -2534,6 +2547,7 @@ int capgen_train_step_indexed(capgen_t* h, const void* feat_store, int feats_dty
       throw;
     }
     h->in_idx = nullptr;
+    h->dp_check((hipStream_t)stream, loss_out);
   });
 }
 
@@ -2853,6 +2867,14 @@ int capgen_dp_comm_info(capgen_t* h, int* nranks, int* rank) {
     }
     if (nranks) *nranks = n;
     if (rank) *rank = r;
+  });
+}
+
+int capgen_dp_check(capgen_t* h, const float* loss, void* stream) {
+  return guarded([&] {
+    set_device(h);
+    require(h->comm != nullptr, "dp_check: no communicator (capgen_dp_init first)");
+    h->dp_check((hipStream_t)stream, loss, /*force=*/true);
   });
 }
 

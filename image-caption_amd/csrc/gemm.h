@@ -65,7 +65,7 @@ struct GemmArgs {
   const int32_t* ln_ids = nullptr;
   int64_t ln_ids_ld = 0;
   int ln_pad = 0;
-  int a_table_rows = 0;  // a_ids: rows of the table A (hazard checker)
+  int a_table_rows = 0;  // a_ids: rows of the table A (the kernel clamps ids into it; hazard checker)
   const void* ln_res = nullptr;
   // register-B path: A rows gathered by index -- row m of the product is A[a_ids[m * a_ids_ld]] (the
   // decode step's word-embedding projection reads the bf16 embedding table directly)

@@ -61,14 +61,17 @@ __global__ void __launch_bounds__(256) breg_kernel(GemmArgs g) {
 #pragma unroll
       for (int f = 0; f < FN; ++f) dst[q][f] = *reinterpret_cast<const bf16x8*>(brow[f] + (int64_t)(b * QB + q) * 512);
   };
-  // A rows past M read row M - 1 (their results are never stored)
+  // A rows past M read row M - 1 (their results are never stored).  Gathered rows: the selection
+  // kernels only produce ids in [0, V); the clamp keeps a foreign id inside the table (gemm.hip
+  // requires a_table_rows > 0 for every gathered launch)
   const bf16* arow[CPT];
   int aoff[CPT];
 #pragma unroll
   for (int c = 0; c < CPT; ++c) {
     const int id = tid + 256 * c, row = id / (KT * 4), ch = id % (KT * 4);
     const int m = min(m0 + row, M - 1);
-    arow[c] = A + (int64_t)(g.a_ids ? g.a_ids[(int64_t)m * g.a_ids_ld] : m) * g.lda + ch * 8;
+    const int ar_ = g.a_ids ? min(max(g.a_ids[(int64_t)m * g.a_ids_ld], 0), g.a_table_rows - 1) : m;
+    arow[c] = A + (int64_t)ar_ * g.lda + ch * 8;
     aoff[c] = row * RB + ((ch ^ (row & 7)) * 16);
   }
   u32x4 ar[AD][CPT];  // A(t) in ar[t % AD], loaded AD - 1 k-tiles before its LDS write

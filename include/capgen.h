@@ -310,9 +310,14 @@ int capgen_dp_set_global_count(capgen_t* h, float count);
  * would (Adam on this rank's chunks only); world <= 1 turns it off. */
 int capgen_dp_sync_adam_state(capgen_t* h);
 /* The engine communicator's size and this rank (ncclCommCount / ncclCommUserRank; 0 / 0 before
- * capgen_dp_init).  At world > 1 the FIRST capgen_train_step also checks, once, that every rank holds
- * the same global non-pad count and loss (max == min over the ranks) and fails the step otherwise. */
+ * capgen_dp_init).  At world > 1 the FIRST capgen_train_step / capgen_train_step_indexed also checks,
+ * once, that every rank holds the same global non-pad count and loss (max == min over the ranks; the
+ * loss the step wrote to loss_out, or its internal loss when loss_out was null) and fails the step
+ * otherwise.  capgen_dp_check runs that same exchange now, at any world size (collective: every rank
+ * calls it; needs capgen_dp_init and a train step before it; loss null = the buffer the last forward
+ * wrote its loss to) -- the world-1 rehearsal of the check. */
 int capgen_dp_comm_info(capgen_t* h, int* nranks, int* rank);
+int capgen_dp_check(capgen_t* h, const float* loss, void* stream);
 /* Exact, order-independent checksum of the f32 parameter arena (sum of the bit patterns times
  * (2 i + 1), mod 2^64; synchronous): equal parameters give equal values on every rank. */
 int capgen_params_checksum(capgen_t* h, uint64_t* out);

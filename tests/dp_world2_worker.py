@@ -1,10 +1,19 @@
 """One rank of a data-parallel run of the engine (launched by tests/test_gpu_dp_world2.py
 through torch.distributed.run; rank r on GPU r).
 
-Each rank trains the fp32 engine for three steps on its half of a fixture batch through the engine's
-own RCCL communicator (count all-reduce, per-bucket gradient all-reduce or ZeRO-1 reduce-scatter /
-all-gather, engine.hip) and writes its parameters, losses, checksum and communicator size to
-<out>.r<rank>.npz.  torch.distributed (gloo) is only the bootstrap channel for the unique id."""
+Each rank trains the fp32 engine through the engine's own RCCL communicator (count all-reduce,
+per-bucket gradient all-reduce or ZeRO-1 reduce-scatter / all-gather, engine.hip) and writes its
+parameters, losses, checksum and communicator size to <out>.r<rank>.npz.  torch.distributed (gloo)
+is only the bootstrap channel for the unique id.
+
+Batches:
+- a fixture tag ("c1"): rank r takes its 1/world slice of the fixture batch (fixture weights);
+- "c3": SURVEY §8(e)'s C3 -- the C2 model (reference init, seed 0), 64 images per rank, rank r's
+  batch = bench.py's synthetic_batch(seed=1000 + r); also writes the parameters after step 1.
+
+After the steps every rank runs the forced consistency check (capgen_dp_check) with the loss
+tensor the last step wrote and with the engine's internal loss: the exchange the first step runs by
+itself at world > 1, here at any world size (at world 1 this is its only run)."""
 import os
 import sys
 
@@ -17,6 +26,12 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 
+def c3_batch(cfg, rank, B=64):
+    from capgen.synthetic import synthetic_batch
+    return synthetic_batch(B, 36, cfg.encode_dim_features, cfg.encode_dim_positions, 20, cfg.num_vocab,
+                           seed=1000 + rank)
+
+
 def main():
     tag, zero, steps, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
@@ -24,24 +39,41 @@ def main():
     from capgen import _lib
     from capgen.dp import init_engine_dp
     from capgen.engine import Engine
-    from capgen.params import fixture_state_dict
-    from golden_util import fixture_inputs, load_fixture
 
     _lib.set_knob("ZERO", zero)
     dev = f"cuda:{rank}"
-    cfg, seed, z = load_fixture(tag)
-    f, p, c = (t.to(dev) for t in fixture_inputs(z))
+    if tag == "c3":
+        from capgen.config import preset
+        from capgen.params import reference_init_state_dict
+        cfg = preset("C2")
+        sd = reference_init_state_dict(cfg, seed=0, with_buffer=False)
+        f, p, c = (t.to(dev) for t in c3_batch(cfg, rank))
+    else:
+        from capgen.params import fixture_state_dict
+        from golden_util import fixture_inputs, load_fixture
+        cfg, seed, z = load_fixture(tag)
+        sd = fixture_state_dict(cfg, seed=seed, with_buffer=False)
+        f, p, c = (t.to(dev) for t in fixture_inputs(z))
+        h = c.shape[0] // world
+        sl = slice(rank * h, (rank + 1) * h)
+        f, p, c = f[sl], p[sl], c[sl]
     e = Engine(cfg.replace(dtype="fp32"), dev)
-    e.load_state_dict(fixture_state_dict(cfg, seed=seed, with_buffer=False))
+    e.load_state_dict(sd)
     e.set_training(False)
     init_engine_dp(e, rank, world)
-    h = c.shape[0] // world
-    sl = slice(rank * h, (rank + 1) * h)
-    losses = [e.train_step(f[sl], p[sl], c[sl]).item() for _ in range(steps)]
+    losses, params1 = [], None
+    for i in range(steps):
+        losses.append(e.train_step(f, p, c).item())
+        if i == 0 and tag == "c3":
+            torch.cuda.synchronize()
+            params1 = e.params_arena()
+    e.dp_check(e._loss)  # forced: count and loss agree over the ranks
+    e.dp_check(None)     # the internal-loss form of the same exchange
     torch.cuda.synchronize()
+    extra = {"params1": params1} if params1 is not None else {}
     np.savez(f"{out}.r{rank}.npz", params=e.params_arena(), losses=np.array(losses),
              checksum=np.array([e.params_checksum()], dtype=np.uint64),
-             comm=np.array([e.dp_comm_info()[0]]))
+             comm=np.array([e.dp_comm_info()[0]]), **extra)
     dist.barrier()
     e.close()
     dist.destroy_process_group()

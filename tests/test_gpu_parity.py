@@ -799,6 +799,32 @@ def test_decode_tiles_follow_weight_updates():
     assert torch.equal(e.beam(fd, pd, 5), fresh.beam(fd, pd, 5))
 
 
+def test_decode_tiles_follow_graph_replayed_steps():
+    """Whole-step graph mode (set_graph(True)): from the second step on, Adam runs inside a graph
+    replay with no host code, so the weight version the decode tiles key on must move with every
+    replay (engine.hip, `++wver` beside hipGraphLaunch).  Decode after step 1 (tiles built), then
+    three more replayed steps, then greedy and beam must equal a fresh engine's holding the trained
+    weights."""
+    from capgen.engine import Engine
+    _, cfg, sd, e, f, p, c = _c2_setup(B=64, dtype="bf16", weights="fixture")
+    fd, pd, cd = f.to(DEV).bfloat16(), p.to(DEV), c.to(DEV)
+    e.set_training(False)
+    e.set_graph(True)
+    e.train_step(fd, pd, cd)
+    e.greedy(fd, pd)  # decode tiles built at the weights of step 1
+    for _ in range(3):
+        e.train_step(fd, pd, cd)
+    torch.cuda.synchronize()
+    fresh = Engine(cfg.replace(dtype="bf16"), DEV)
+    fresh.set_training(False)
+    fresh.set_params_arena(e.params_arena())
+    i_e, _ = e.greedy(fd, pd)
+    i_f, _ = fresh.greedy(fd, pd)
+    assert torch.equal(i_e, i_f)
+    assert torch.equal(e.beam(fd, pd, 5), fresh.beam(fd, pd, 5))
+    fresh.close()
+
+
 def test_breg_decode_tracks_ring_decode(set_knob):
     """bf16 C4-style decode with the decoder Linears on the register-B GEMM (CAPGEN_BREG_DECODE,
     default on) against the LDS-ring GEMM: the products differ only in summation order inside the
