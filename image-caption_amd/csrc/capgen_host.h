@@ -25,7 +25,7 @@ inline void require(bool ok, const std::string& what) {
 enum class Knob : int {
   FusedCe, GroupDw, FusedQkv, FusedAttnBwd, ColsumSide, DecodeCrossMfma, SlabDecode, DecodeGroupLds, AttnWave,
   CeVec8, BregDecode, DecodeLnFold, OverlapFront, OverlapDec0, StripeClear, BucketBlocks, Zero, FwdGraph, FwdSplit, GenGraph, Streams,
-  EventFence, Autotune, AutotuneLog,
+  EventFence, DeferLoss, FrontJoin, Autotune, AutotuneLog,
   Skip, DebugDropJoin, SplitkProto, AllowPartialLines, DwVariant, HostTiming,  // debug build only
   Count
 };

@@ -416,6 +416,14 @@ struct capgen_engine {
   bool fused_ce_on = knob(Knob::FusedCe) != 0;
   bool need_logits = false;  // the next forward must materialise the f32 logits (SCST sampling)
   bool fused_ce() const { return fused_ce_on && !need_logits && act == DType::BF16 && L_().V % 4 == 0; }
+  // train step without a collective or FocalLoss: the CE gradient scale 1/count comes from the caption
+  // prep (the count is known there), so the loss finalisation (the mean of the loss rows) leaves the
+  // critical stream: the step's forward skips it and its backward issues it on es2 after the first
+  // fork (pending_loss).  With a count all-reduce or FocalLoss the scale needs the finalisation first.
+  bool loss_deferrable() const { return !comm && !count_override && !cfg.focal_loss && defer_loss_on; }
+  bool defer_loss_on = knob(Knob::DeferLoss) != 0;
+  int front_join = knob(Knob::FrontJoin);  // encoder block before which the forward joins the decoder front
+  float* pending_loss = nullptr;  // set by train_step: the backward finalises the loss into it on es2
   static constexpr bool direct_on = true;
 
   // diagnostic in-kernel timestamps (capgen_debug_stamps): every GEMM / LayerNorm / attention
@@ -881,7 +889,8 @@ struct capgen_engine {
   // ------------------------------------------------------------------------------------
   // forward (model.py:79-98).  Always keeps the activations needed by backward.
   void forward(const void* feats, DType ft, const float* pos, const int32_t* caps, int B, int N, int T,
-               float* loss_out, bool drop_on, hipStream_t s) {
+               float* loss_out, bool drop_on, hipStream_t s, bool defer_loss = false) {
+    const bool defer = defer_loss && loss_deferrable();
     require(B >= 1 && N >= 1 && T >= 2, "forward: need B>=1, N>=1, T>=2");
     require(N <= 64 && T - 1 <= L.maxlen - 1, "forward: N must be <= 64 and T <= max_length");
     const int Lq = T - 1, Me = B * N, Md = B * Lq, d = L.d, dd = L.dd;
@@ -897,7 +906,7 @@ struct capgen_engine {
     // caption ids / targets / count: with the decoder front on es2 (and no count all-reduce, which
     // stays on the critical stream) the prep runs there too, first thing of the front
     const bool caps_front = overlap_front && es2 != s && !comm;
-    if (!caps_front) prepare_captions(caps, B, T, cfg.pad_idx, a.ids, a.tgt, a.count, s);
+    if (!caps_front) prepare_captions(caps, B, T, cfg.pad_idx, a.ids, a.tgt, a.count, s, nullptr, defer ? a.grad_scale : nullptr);
     if (comm) {
       if (count_override) {
         if (hz::active()) hz::op(s, "count_copy", {hz::wr(a.count, 4)});
@@ -947,7 +956,7 @@ struct capgen_engine {
     if (front) {
       if (cap_split) cap_cut(s, 0, es2);
       else dep(s, es2, ev_ff);
-      if (caps_front) prepare_captions(caps, B, T, cfg.pad_idx, a.ids, a.tgt, a.count, es2);
+      if (caps_front) prepare_captions(caps, B, T, cfg.pad_idx, a.ids, a.tgt, a.count, es2, nullptr, defer ? a.grad_scale : nullptr);
       dec_embed(a.tmpf, es2);
       dec_self_half(0, a.tmpf, es2, true);
       if (cap_split) cap_cut(es2, 1, s);
@@ -963,15 +972,21 @@ struct capgen_engine {
       ln.y = a.X[0], ln.v_save = a.ev0, ln.mean = a.em0, ln.rstd = a.er0;
       linear_ln(a.Aenc, L.Kp, L.enc_emb_W, L.Kp, Me, d, L.Kp, ln, s);
     }
-    for (int l = 0; l < L.Le; ++l)
+    // where the critical stream joins the decoder front (eager / single graph): before encoder block
+    // front_join (Le + 1: before the decoder, its first reader)
+    const int fj = std::max(0, std::min(front_join, L.Le + 1));
+    for (int l = 0; l < L.Le; ++l) {
+      if (front && !cap_split && l == fj) hz::wait(s, ev_fj);
       enc_layer_fwd(L.enc[l], a.enc[l], a.X[l], a.X[l + 1], B, N, cfg.encode_mask ? a.valid : nullptr, l, drop_on, s);
+    }
+    if (front && !cap_split && fj == L.Le) hz::wait(s, ev_fj);
     // cross-attention K/V of every decoder block in one GEMM over the encoder output
     linear(a.X[L.Le], d, L.Wkv_all, d, a.KV, (int64_t)L.Ld * 2 * dd, act, Me, L.Ld * 2 * dd, d, nullptr, 0, s);
 
     // ---- decoder (model.py:419-459) ----
     if (front && cap_split) cap_cut(s, 2, s);
-    else if (front) hz::wait(s, ev_fj);
-    else dec_embed(a.tmp, s);
+    else if (front && fj > L.Le) hz::wait(s, ev_fj);
+    else if (!front) dec_embed(a.tmp, s);
     const int64_t kvld = (int64_t)L.Ld * 2 * dd;
     for (int l = 0; l < L.Ld; ++l) {
       const auto& w = L.dec[l];
@@ -1029,7 +1044,7 @@ struct capgen_engine {
       nccl_op(s, "allreduce(ce)", a.loss_ce, 4);
       NCCL_CHECK(ncclAllReduce(a.loss_ce, a.loss_ce, 1, ncclFloat, ncclSum, comm, s));
       loss_finalize(nullptr, 0, a.count, cfg.focal_loss, lo, a.grad_scale, s, a.loss_ce);
-    } else {
+    } else if (!defer) {
       loss_finalize(a.loss_row, Md, a.count, cfg.focal_loss, lo, a.grad_scale, s);
     }
     stamp_fwd_end = stamp_next;
@@ -1400,13 +1415,20 @@ struct capgen_engine {
       return lnb_desc(Me, d, dy, a.ev0, a.em0, a.er0, L.enc_lng, L.enc_lnb, -1, RowMask{}, Drop{}, nullptr, a.gAe);
     };
 
-    // classifier: dlogits are unscaled (softmax - onehot); grad_scale folds 1/count (+focal)
-    fork(s);
-    if (emb_zero_side) memset_async(grads + L.n_dense, (L.enc_lng - L.n_dense) * sizeof(float), es2);
-    column_sum(a.dlogits, Md, L.V, L.V, 1.f, a.grad_scale, GS(L.bc), act, es2, NSTRIPE, n_small);
+    // classifier: dlogits are unscaled (softmax - onehot); grad_scale folds 1/count (+focal).  The
+    // critical stream goes straight from the forward into the dX GEMM: the side work (weight and bias
+    // gradients, the embedding-gradient clear, a deferred loss finalisation) forks after it, with the
+    // flush the classifier's bucket needs anyway (one event record on the critical stream, not two)
     dw_side(a.dlogits, L.V, dec_out(), dd, L.Wc, dd, Md, L.V, dd, a.grad_scale, s);
     linear_dx(a.dlogits, L.V, L.Wc, dd, a.gOut, dd, Md, L.V, dd, 0, nullptr, a.grad_scale, s);
-    bucket(L.Wc, L.n_dense - L.Wc, s);  // flushed after the dX GEMM above: it reads Wc
+    flush(s);  // es2: the classifier dW (the bucket below waits for it: it reads Wc's gradient)
+    bucket(L.Wc, L.n_dense - L.Wc, s, /*sync=*/false);
+    if (emb_zero_side) memset_async(grads + L.n_dense, (L.enc_lng - L.n_dense) * sizeof(float), es2);
+    column_sum(a.dlogits, Md, L.V, L.V, 1.f, a.grad_scale, GS(L.bc), act, es2, NSTRIPE, n_small);
+    if (pending_loss) {  // the mean CE (model.py:96); grad_scale was written by the caption prep
+      loss_finalize(a.loss_row, Md, a.count, 0, pending_loss, nullptr, es2);
+      pending_loss = nullptr;
+    }
 
     const int64_t kvld = (int64_t)L.Ld * 2 * dd;
     void* gO = a.gOut;
@@ -1596,6 +1618,11 @@ struct capgen_engine {
                                 std::to_string(hv[2]) + ", min " + std::to_string(hv[3]) + ")");
   }
 
+  // after a train step's forward (eager, captured or replayed): its deferred loss goes to `loss`
+  void set_pending_loss(float* loss) {
+    pending_loss = loss_deferrable() ? (loss ? loss : a.loss) : nullptr;
+    if (pending_loss) last_loss = pending_loss;
+  }
   void train_step(const void* f, DType ft, const float* pos, const int32_t* caps, int B, int N, int T, float* loss,
                   hipStream_t cs) {
     ensure_acts(B, N, T);
@@ -1607,6 +1634,7 @@ struct capgen_engine {
       hz::set_critical(cs);
       launch_fwd(cs);
       fB = B, fN = N, fT = T, fwd_drop = training;  // host state forward() would have set
+      set_pending_loss(loss);
       backward(cs, /*step_params=*/true);
       crit = nullptr;
       hz::record(ev_out, cs);
@@ -1619,7 +1647,8 @@ struct capgen_engine {
       static double tf = 0, tb = 0;
       static int nsteps = 0;
       auto t0 = std::chrono::steady_clock::now();
-      forward(f, ft, pos, caps, B, N, T, loss, training, es);
+      forward(f, ft, pos, caps, B, N, T, loss, training, es, /*defer_loss=*/true);
+      set_pending_loss(loss);
       auto t1 = std::chrono::steady_clock::now();
       backward(es, /*step_params=*/true);  // + bucketed RCCL all-reduce (DP) and Adam
       if (host_timing) {
@@ -1652,7 +1681,7 @@ struct capgen_engine {
         cap_split = fwd_split() && overlap_front && es2 != es;
         CAPGEN_HIP(hipStreamBeginCapture(es, hipStreamCaptureModeThreadLocal));
         try {
-          forward(f, ft, pos, caps, B, N, T, loss, training, es);
+          forward(f, ft, pos, caps, B, N, T, loss, training, es, /*defer_loss=*/true);
         } catch (...) {
           (void)hipStreamEndCapture(es, &graph);
           if (graph) (void)hipGraphDestroy(graph);
@@ -1683,6 +1712,7 @@ struct capgen_engine {
       launch_fwd(es);
       auto t1 = std::chrono::steady_clock::now();
       fB = B, fN = N, fT = T, fwd_drop = training;  // host state forward() would have set
+      set_pending_loss(loss);
       backward(es, /*step_params=*/true);
       if (host_timing) {
         auto t2 = std::chrono::steady_clock::now();

@@ -53,6 +53,8 @@ constexpr KnobDef kDefs[] = {
     {Knob::GenGraph, "GEN_GRAPH", 0, false},          // decode steps as captured graphs
     {Knob::Streams, "STREAMS", 3, false},             // engine streams (3, 2 or 1)
     {Knob::EventFence, "EVENT_FENCE", 1, false},      // 1 no system fence, 2 device release, 0 HIP default
+    {Knob::DeferLoss, "DEFER_LOSS", 1, false},        // train step's loss mean on es2 (0: on the critical stream)
+    {Knob::FrontJoin, "FRONT_JOIN", 99, false},       // forward joins the decoder front before encoder block N (> Le: before the decoder)
     {Knob::Autotune, "AUTOTUNE", 1, false},           // time GEMM shapes the tune table lacks
     {Knob::AutotuneLog, "AUTOTUNE_LOG", 0, false},    // print tuning decisions
     // debug build only

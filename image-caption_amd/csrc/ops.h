@@ -56,9 +56,10 @@ void layernorm_bwd(const LnBwd& a, DType t, hipStream_t s);
 void pack_encoder_input(const void* feats, DType feats_t, const float* pos, int M, int F, int P, int Kp,
                         void* out, DType out_t, uint8_t* valid, hipStream_t s, const int32_t* img_idx = nullptr,
                         int N = 0, int n_img = 0, uint64_t* seed_bump = nullptr);
-// caps [B][T] -> ids_in [B][T-1], tgt [B][T-1]; count = #(tgt != pad) as f32   (model.py:88-89)
+// caps [B][T] -> ids_in [B][T-1], tgt [B][T-1]; count = #(tgt != pad) as f32   (model.py:88-89);
+// inv_count (optional): 1 / count, the CE mean's gradient scale (model.py:96)
 void prepare_captions(const int32_t* caps, int B, int T, int pad, int32_t* ids_in, int32_t* tgt,
-                      float* count, hipStream_t s, uint64_t* seed_bump = nullptr);
+                      float* count, hipStream_t s, uint64_t* seed_bump = nullptr, float* inv_count = nullptr);
 // out[m] = table[ids[m]] (f32 table -> T)                                      (model.py:432)
 // (table_rows: rows of the table, for the hazard checker's byte ranges only)
 void embedding_gather(const float* table, const int32_t* ids, int64_t ids_ld, int M, int d, void* out, DType t,
@@ -81,7 +82,8 @@ void cross_entropy_rows(const float* logits, const int32_t* tgt, int M, int V, i
 void ce_finish(const float2* stats, int64_t ld, const float* tlogit, const int32_t* tgt, int M, int V, int pad,
                float* loss_row, bf16* dl, hipStream_t s);
 // loss = sum(loss_row)/count (or FocalLoss of it); grad_scale = dloss/d(logit sums).
-// ce_in: the mean CE is given (all-reduced partials); partial: write sum(loss_row)/count only.
+// ce_in: the mean CE is given (all-reduced partials); partial: write sum(loss_row)/count only;
+// grad_scale null: the loss only (the scale was written elsewhere, e.g. by prepare_captions).
 void loss_finalize(const float* loss_row, int M, const float* count, int focal, float* loss_out,
                    float* grad_scale, hipStream_t s, const float* ce_in = nullptr, int partial = 0);
 // Adam (torch.optim.Adam semantics).  step_buf: int64 step counter (incremented here).

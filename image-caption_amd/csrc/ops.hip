@@ -377,7 +377,7 @@ void pack_encoder_input(const void* feats, DType ft, const float* pos, int M, in
 }
 
 __global__ void prep_caps_kernel(const int32_t* __restrict__ caps, int B, int T, int pad, int32_t* ids_in,
-                                 int32_t* tgt, float* count, uint64_t* seed_bump) {
+                                 int32_t* tgt, float* count, uint64_t* seed_bump, float* inv_count) {
   __shared__ int cnt;
   if (threadIdx.x == 0) cnt = 0;
   // the step's dropout seed advance (bump_seed) rides along: no kernel in this launch reads it
@@ -395,16 +395,17 @@ __global__ void prep_caps_kernel(const int32_t* __restrict__ caps, int B, int T,
   atomicAdd(&cnt, local);
   __syncthreads();
   if (threadIdx.x == 0) *count = (float)cnt;
+  if (inv_count && threadIdx.x == 0) *inv_count = 1.f / (float)cnt;  // as loss_finalize's 1.f / n
 }
 
 void prepare_captions(const int32_t* caps, int B, int T, int pad, int32_t* ids_in, int32_t* tgt, float* count,
-                      hipStream_t s, uint64_t* seed_bump) {
+                      hipStream_t s, uint64_t* seed_bump, float* inv_count) {
   if (hz::active()) {
     using namespace hz;
     op(s, "prep_captions", {rd(caps, (int64_t)B * T * 4), wr(ids_in, (int64_t)B * (T - 1) * 4),
-                            wr(tgt, (int64_t)B * (T - 1) * 4), wr(count, 4), wr(seed_bump, 8)});
+                            wr(tgt, (int64_t)B * (T - 1) * 4), wr(count, 4), wr(seed_bump, 8), wr(inv_count, 4)});
   }
-  prep_caps_kernel<<<1, 1024, 0, s>>>(caps, B, T, pad, ids_in, tgt, count, seed_bump);
+  prep_caps_kernel<<<1, 1024, 0, s>>>(caps, B, T, pad, ids_in, tgt, count, seed_bump, inv_count);
   CAPGEN_HIP(hipGetLastError());
 }
 
@@ -764,10 +765,10 @@ __global__ void loss_finalize_kernel(const float* __restrict__ loss_row, int M, 
       const float pt = expf(-ce);
       const float om = 1.f - pt;
       *loss_out = om * om * ce;
-      *grad_scale = (2.f * om * pt * ce + om * om) / n;
+      if (grad_scale) *grad_scale = (2.f * om * pt * ce + om * om) / n;
     } else {
       *loss_out = ce;
-      *grad_scale = 1.f / n;
+      if (grad_scale) *grad_scale = 1.f / n;
     }
   }
 }
