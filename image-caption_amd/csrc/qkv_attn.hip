@@ -41,6 +41,29 @@ constexpr int QKB = 4;        // k-steps per register batch of weight fragments
 __device__ __forceinline__ int xswz(int row, int chunk) { return chunk ^ (row & 15); }
 __device__ int32_t g_qa_dummy[64];  // target of the absent key-mask inputs (never used as a value)
 
+// The image's rows of a [L][512] bf16 operand (X in the front, dA in the backward) into the LDS
+// staging area by LDS-DMA (round 6): one buffer_load_dwordx4 ... lds per 1-KB row, lane l's 16 B
+// landing at slot l of the row -- slot l holds chunk l ^ (row & 15), the XOR swizzle applied through
+// the source offset.  Rows >= L get an offset past the buffer's num_records (zeros land), so every
+// staged row up to 16 LT is written.  Nothing passes through VGPRs: the register staging it replaces
+// held the image's rows in 4 LT uint4 per lane (48 VGPRs at LT = 3) across the weight loads.  The
+// issuing wave's s_waitcnt vmcnt(0) + a workgroup barrier make the rows visible (the caller).
+// `s_nop 4`: the VALU-written M0 / voff before an LDS-DMA need wait states hipcc does not pad into an
+// asm statement (gemm_tile.h Op::dma).
+template <int LT>
+__device__ __forceinline__ void dma_rows(const bf16* rows, int64_t ld, int L, char* xs, int w, int lane) {
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(rows), 0, (int)((int64_t)L * ld * 2), 0x00020000);
+#pragma unroll
+  for (int j = 0; j < 4 * LT; ++j) {
+    const int row = w + 4 * j;
+    const uint32_t voff = row < L ? (uint32_t)(((int64_t)row * ld + (lane ^ (row & 15)) * 8) * 2) : 0x80000000u;
+    asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(rs), "s"(0u),
+                 "{m0}"((unsigned)(uintptr_t)(xs + row * (QD * 2)))
+                 : "memory");
+  }
+}
+
 __device__ __forceinline__ void bf8_to_f(const uint4& u, float (&f)[8]) {
   const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
@@ -84,15 +107,7 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
 #pragma unroll
     for (int f = 0; f < NF; ++f) bq[0][kk][f] = *reinterpret_cast<const bf16x8*>(wrow[f] + 512 * kk);
   {
-    constexpr int CH = LT * 16 * QD / 8;  // 16-B chunks of the staged rows
-    constexpr int PER = CH / 256;
-    uint4 v[PER];
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int c = tid + 256 * u, row = c / (QD / 8), ch = c % (QD / 8);
-      v[u] = row < L ? *reinterpret_cast<const uint4*>(xb + (int64_t)min(row, L - 1) * a.ldx + ch * 8)
-                                : uint4{0u, 0u, 0u, 0u};
-    }
+    dma_rows<LT>(xb, a.ldx, L, xs, w, lane);  // X rows -> LDS, nothing through registers
     // cross attention: K / V head slices from memory (rows < Lk)
     uint4 kv[2][2];
     if constexpr (NP == 1) {
@@ -122,11 +137,6 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
 #pragma unroll
     for (int u = 0; u < NP * IMG / 16 / 256; ++u)
       reinterpret_cast<uint4*>(sm)[tid + 256 * u] = uint4{0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int c = tid + 256 * u, row = c / (QD / 8), ch = c % (QD / 8);
-      *reinterpret_cast<uint4*>(xs + row * (QD * 2) + xswz(row, ch) * 16) = row < L ? v[u] : uint4{0u, 0u, 0u, 0u};
-    }
     if constexpr (NP == 1) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -146,6 +156,7 @@ __global__ void __launch_bounds__(256) qkv_attn_kernel(QkvAttn a) {
   for (int i = 0; i < LT; ++i)
 #pragma unroll
     for (int f = 0; f < NF; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's X rows have landed (and its weights)
   __syncthreads();  // X staged
 #pragma unroll
   for (int grp = 0; grp < QKS / QKB; ++grp) {
@@ -227,15 +238,7 @@ __global__ void __launch_bounds__(256) qkv_attn_bwd_kernel(QkvBwd a) {
   bf16x8 bq[QKS];
 #pragma unroll
   for (int ks = 0; ks < QKS; ++ks) bq[ks] = *reinterpret_cast<const bf16x8*>(wrow + 512 * ks);
-  constexpr int CH = LT * 16 * QD / 8, PER = CH / 256;
-  const bf16* xb = a.dA + (int64_t)b * L * a.ldda;
-  uint4 xv[PER];
-#pragma unroll
-  for (int u = 0; u < PER; ++u) {
-    const int c = tid + 256 * u, row = c / (QD / 8), ch = c % (QD / 8);
-    xv[u] = row < L ? *reinterpret_cast<const uint4*>(xb + (int64_t)min(row, L - 1) * a.ldda + ch * 8)
-                               : uint4{0u, 0u, 0u, 0u};
-  }
+  dma_rows<LT>(a.dA + (int64_t)b * L * a.ldda, a.ldda, L, xs, w, lane);  // dA rows -> LDS (no registers)
   const int bk = g.kv_bmod ? b % g.kv_bmod : b;
   const bf16* src[3] = {reinterpret_cast<const bf16*>(g.k) + (int64_t)bk * g.k_bs + h * DK,
                         reinterpret_cast<const bf16*>(g.q) + (int64_t)b * g.q_bs + h * DK,
@@ -259,14 +262,10 @@ __global__ void __launch_bounds__(256) qkv_attn_bwd_kernel(QkvBwd a) {
     kvl = opaque(g.key_valid ? g.key_valid : reinterpret_cast<const uint8_t*>(g_qa_dummy))[
         g.key_valid ? (int64_t)bk * g.kv_bs + j : lane];
   }
-  // dA rows -> LDS (rows >= L zero), the dO image zeroed (rows >= 16 LT are never projected)
-#pragma unroll
-  for (int u = 0; u < PER; ++u) {
-    const int c = tid + 256 * u, row = c / (QD / 8), ch = c % (QD / 8);
-    *reinterpret_cast<uint4*>(xs + row * (QD * 2) + xswz(row, ch) * 16) = row < L ? xv[u] : uint4{0u, 0u, 0u, 0u};
-  }
+  // the dO image zeroed (rows >= 16 LT are never projected); the dA rows (rows >= L zero) landing by DMA
 #pragma unroll
   for (int u = 0; u < 2; ++u) reinterpret_cast<uint4*>(dOimg)[tid + 256 * u] = uint4{0u, 0u, 0u, 0u};
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's dA rows have landed (and its loads)
   __syncthreads();
   f32x4 acc[LT];
 #pragma unroll
