@@ -102,7 +102,8 @@ def _pmc_traffic():
     path = found[-1]  # the newest round's passes
     with open(path) as fh:
         d = json.load(fh)
-    return {"bytes_per_step": d["hbm_bytes_per_step"], "source": os.path.relpath(path, REPO)}
+    return {"bytes_per_step": d["hbm_bytes_per_step"], "source": os.path.relpath(path, REPO),
+            "commit": d.get("commit", "unrecorded")}
 
 
 def cpu_baseline(cfg, steps=5, warmup=2, c1_steps=50):
@@ -269,10 +270,14 @@ def main():
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_BF16_TFLOPS, 5),
                      "traffic": traffic["bytes_per_step"] if traffic else None,
+                     # the commit of the tree the PMC passes profiled: a train path changed since then
+                     # makes `traffic` stale, visibly
+                     "traffic_commit": traffic["commit"] if traffic else None,
                      "scope": f"one train step = {B} images x {gfl_img:.5f} GFLOP/image "
                               f"algorithmic (SURVEY §8(d)); step time {step_ms_events:.4f} ms from HIP events "
                               f"on the launch stream" + (f"; traffic = HBM bytes/step from the committed PMC "
-                                                         f"summary {traffic['source']} (not measured in this run)"
+                                                         f"summary {traffic['source']} (not measured in this run; "
+                                                         f"profiled tree: commit {traffic['commit']})"
                                                          if traffic else "")},
         "final_loss": round(final_loss, 5),
         "dp_check": dp,

@@ -56,6 +56,15 @@ ALG = {  # class -> (GFLOP, algorithmic GB) per step
 }
 
 
+def floors():
+    """class -> per-XCD panel floor GB (tools/gemm_floor.py: every XCD's L2 fetches each operand panel
+    its tiles read once, for the kernel's tile-to-XCD map and the autotuned tiles)."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import gemm_floor as gf
+    t = gf.tune_table()
+    return {"GEMM dX (NN)": gf.class_floor(gf.DX, t)[1] / 1e9, "GEMM fwd (NT)": gf.class_floor(gf.FWD, t)[1] / 1e9}
+
+
 def klass(name):
     if "grouped" in name:
         return "GEMM dW (TN)"
@@ -113,15 +122,18 @@ def main():
             mf[k][0] += float(r["Counter_Value"])
         elif r["Counter_Name"].startswith("GRBM_GUI_ACTIVE"):
             mf[k][1] += float(r["Counter_Value"])
+    fl = floors()
     print(f"{'class':16s} {'n/step':>6s} {'us/step':>8s} {'GFLOP':>7s} {'TF/s':>6s} {'alg GB':>7s} "
-          f"{'PMC GB':>7s} {'PMC/alg':>7s} {'MFMA busy':>9s}")
+          f"{'PMC GB':>7s} {'PMC/alg':>7s} {'floor GB':>8s} {'PMC/floor':>9s} {'MFMA busy':>9s}")
     for k in sorted(t, key=lambda k: -t[k][1]):
         gf, ab = ALG.get(k, (0, 0))
         pb = (by[k][0] + by[k][1]) / 1e9
         busy = mf[k][0] / (mf[k][1] * 256 / 8 * 4) if mf[k][1] else 0.0  # per-XCD GRBM cycles x 32 CUs x 4 SIMDs
         tfs = gf / t[k][1] * 1e3 if gf else 0.0  # GFLOP / us = PFLOP/s
+        f = fl.get(k)
+        fcol = f"{f:8.3f} {pb / f:9.2f}" if f else f"{'-':>8s} {'-':>9s}"
         print(f"{k:16s} {t[k][0]:6.1f} {t[k][1]:8.1f} {gf:7.1f} {tfs:6.0f} {ab:7.3f} {pb:7.3f} "
-              f"{(pb / ab if ab else 0):7.2f} {busy:9.4f}")
+              f"{(pb / ab if ab else 0):7.2f} {fcol} {busy:9.4f}")
 
 
 if __name__ == "__main__":

@@ -12,6 +12,7 @@ import collections
 import csv
 import glob
 import json
+import os
 import sys
 
 
@@ -46,7 +47,10 @@ def main():
         agg[short(r["Kernel_Name"])][1] += float(r["Counter_Value"]) * 1024 / nw
     rd = sum(v[0] for v in agg.values())
     wr = sum(v[1] for v in agg.values())
-    out = {"hbm_bytes_per_step": round(rd + wr), "read_bytes_per_step": round(rd), "write_bytes_per_step": round(wr),
+    # the commit the profiled tree was (tools/round_profile.sh passes it: the GPU box has no .git), so a
+    # bench line quoting this file shows which code its traffic belongs to
+    out = {"commit": os.environ.get("CAPGEN_COMMIT", "unknown"),
+           "hbm_bytes_per_step": round(rd + wr), "read_bytes_per_step": round(rd), "write_bytes_per_step": round(wr),
            "steps_averaged": [nf, nw], "correction": "FETCH_SIZE x2 (gfx950 wide-read), kB x1024",
            "per_kernel_class": {k: {"read": round(v[0]), "write": round(v[1])}
                                 for k, v in sorted(agg.items(), key=lambda kv: -(kv[1][0] + kv[1][1]))}}
