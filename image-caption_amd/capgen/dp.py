@@ -1,9 +1,10 @@
 """Data parallel over RCCL/xGMI: one process per GPU, replicated
 parameters, one gradient all-reduce per step inside the engine, exact global-mean CE.
 
-The RCCL communicator lives in libcapgen (so the all-reduce sits in the captured step
-graph, on the engine stream); torch.distributed is only the bootstrap channel that
-carries rank 0's 128-byte unique id.
+The RCCL communicator lives in libcapgen (the count / CE all-reduces on the engine's critical
+stream, the gradient buckets' reduce-scatter / all-gather on its bucket stream; at world > 1 the
+forward is issued eagerly, so every collective is a plain stream call); torch.distributed is only
+the bootstrap channel that carries rank 0's 128-byte unique id.
 """
 from __future__ import annotations
 

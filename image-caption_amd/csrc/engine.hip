@@ -298,7 +298,11 @@ struct capgen_engine {
   bool graph_on = false;
   hipGraphExec_t gexec = nullptr;
   // eager step mode: the forward alone as a linear graph (CAPGEN_FWD_GRAPH=0 disables)
-  bool fwd_graph_on = knob(Knob::FwdGraph) != 0;
+  // (1: at world size 1 -- its RCCL count / CE all-reduces, if any, capture into the graph; at world > 1
+  // the forward is issued eagerly, the collectives as plain stream calls: the multi-rank path keeps
+  // RCCL's standard usage, and eager vs graph measured level on the GPU; 2: the graph at any world size)
+  int fwd_graph_mode = knob(Knob::FwdGraph);
+  bool fwd_graph_on = fwd_graph_mode != 0;
   hipGraphExec_t fexec = nullptr;
   // split forward graphs (CAPGEN_FWD_SPLIT=1, with the decoder front on es2): the front and the
   // critical chain as separate LINEAR graphs on their own streams.  Under rocprofv3 the one
@@ -1628,7 +1632,7 @@ struct capgen_engine {
     ensure_acts(B, N, T);
     Key k{f, pos, caps, loss, (int)ft, B, N, T, training, in_idx, in_n_img};
     // (the hazard checker's log runs the eager forward: the graph replays the same launches)
-    const bool fwd_graph = fwd_graph_on && !hz::g_log;
+    const bool fwd_graph = fwd_graph_on && !hz::g_log && (world <= 1 || fwd_graph_mode == 2);
     if (direct_on && !graph_on && fwd_graph && !count_override && have_fwd_graph() && fkey == k && cs != es) {
       crit = cs;
       hz::set_critical(cs);

@@ -48,7 +48,7 @@ constexpr KnobDef kDefs[] = {
     {Knob::StripeClear, "STRIPE_CLEAR", 1, false},    // striped partial sums zeroed by their folds
     {Knob::BucketBlocks, "BUCKET_BLOCKS", 1, false},  // transformer blocks per gradient bucket
     {Knob::Zero, "ZERO", 1, false},                   // sharded update at world > 1 (2: also at world 1)
-    {Knob::FwdGraph, "FWD_GRAPH", 1, false},          // forward replayed as one hipGraph
+    {Knob::FwdGraph, "FWD_GRAPH", 1, false},          // forward replayed as one hipGraph at world 1 (2: at any world size)
     {Knob::FwdSplit, "FWD_SPLIT", 0, false},          // split forward graphs
     {Knob::GenGraph, "GEN_GRAPH", 0, false},          // decode steps as captured graphs
     {Knob::Streams, "STREAMS", 3, false},             // engine streams (3, 2 or 1)
