@@ -2743,8 +2743,13 @@ int capgen_debug_copy_buffer(capgen_t* h, int which, void* host_dst, int64_t byt
                      : (which - 128) % 8 == 5 ? h->a.enc[(which - 128) / 8].v2
                      : (which - 128) % 8 == 6 ? (void*)h->a.enc[(which - 128) / 8].m2
                                              : (void*)h->a.enc[(which - 128) / 8].r2)
+              // 200 + l / 216 + l: encoder / decoder block l's FFN hidden activations relu(x W1^T + b1)
+              // (the ReLU mask the backward applies)
+              : which >= 200 && which - 200 < Le ? h->a.enc[which - 200].H
+              : which >= 216 && which - 216 < h->L.Ld ? h->a.dec[which - 216].H
                   : nullptr;
-    require(src != nullptr, "debug_copy_buffer: which in 0..7, 32 + 8 l + 0..4, 80 + 0..Le, 128 + 8 l + 0..7");
+    require(src != nullptr,
+            "debug_copy_buffer: which in 0..7, 32 + 8 l + 0..4, 80 + 0..Le, 128 + 8 l + 0..7, 200 + l, 216 + l");
     hz::host_sync(nullptr);
     CAPGEN_HIP(hipMemcpy(host_dst, src, (size_t)bytes, hipMemcpyDeviceToHost));
   });

@@ -186,7 +186,8 @@ int capgen_debug_gemm_timing_buf(void* dev_buf);
 /* Diagnostic: synchronous copy of an internal buffer to host: 0 tmp, 1 gOut, 2 gRes, 3 cross-K/V
  * gradient, 4-7 the last encoder block's FFN-hidden / FFN-LN / MHA-LN / QKV gradients; 32 + 8 l + j
  * encoder block l's gAf / gH / gA1 / gATT1 / gQKV; 80 + l the encoder activations X[l]; 128 + 8 l + j
- * encoder block l's saved forward tensors (att, v1, m1, r1, Y, v2, m2, r2). */
+ * encoder block l's saved forward tensors (att, v1, m1, r1, Y, v2, m2, r2); 200 + l / 216 + l the
+ * encoder / decoder block l's FFN hidden activations (relu output, the backward's ReLU mask). */
 int capgen_debug_copy_buffer(capgen_t* h, int which, void* host_dst, int64_t bytes);
 
 /* Training step over an HBM-resident feature store (replaces TrainDataset.__getitem__ + the
