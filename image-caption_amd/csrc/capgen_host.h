@@ -24,7 +24,7 @@ inline void require(bool ok, const std::string& what) {
 // libcapgen_debug.so): the product library keeps their defaults.
 enum class Knob : int {
   FusedCe, GroupDw, FusedQkv, FusedAttnBwd, ColsumSide, DecodeCrossMfma, SlabDecode, DecodeGroupLds, AttnWave,
-  CeVec8, BregDecode, DecodeLnFold, OverlapFront, OverlapDec0, StripeClear, BucketBlocks, Zero, FwdGraph, FwdSplit, GenGraph, Streams,
+  CeVec8, BregDecode, DecodeLnFold, FusedBeamStep, OverlapFront, OverlapDec0, StripeClear, BucketBlocks, Zero, FwdGraph, FwdSplit, GenGraph, Streams,
   EventFence, DeferLoss, FrontJoin, Autotune, AutotuneLog,
   Skip, DebugDropJoin, SplitkProto, AllowPartialLines, DwVariant, HostTiming,  // debug build only
   Count

@@ -2060,6 +2060,7 @@ struct capgen_engine {
   // bf16 beam decode: the cross attention of an image's beam rows on the MFMA attention kernel
   // (CAPGEN_DECODE_CROSS_MFMA=0: the grouped VALU decode kernel, attention.hip)
   bool cross_mfma_on = knob(Knob::DecodeCrossMfma) != 0;
+  bool fused_beam_step_on = knob(Knob::FusedBeamStep) != 0;
   // bf16 decode: the classifier epilogue writes slab stats and the greedy / beam selection reads
   // k * 16 logits per row instead of the whole row (CAPGEN_SLAB_DECODE=0: full-row kernels)
   bool slab_decode_on = knob(Knob::SlabDecode) != 0;
@@ -2118,12 +2119,24 @@ struct capgen_engine {
     // position 0: every beam holds <START>; top-k of beam 0's distribution (model.py:148-166)
     beam_kvrow_kernel<<<(R * Tc + 255) / 256, 256, 0, s>>>(g.kvrow2, g.kvrow, Tc, -1, g.ids, B, R);  // [r][0] = r
     dec_step(R, B, N, 0, g.cache, g.ids, false, s);
-    if (slab_decode())
+    // bf16: the selection and the reorder of a step as one launch per image (beam_slab_step:
+    // CAPGEN_FUSED_BEAM_STEP=0 restores the top-k, merge and three reorder launches)
+    const bool fused_step = slab_decode() && fused_beam_step_on && k <= 16 && Tw == Tc;
+    auto fused = [&](int t, const float* prev, int kin, float* out_prob) {
+      beam_slab_step(g.logits, g.dstats, prev, kin, B, L.V, k, decode_logsm, out_prob, g.bsrc, g.btok, g.seq, g.seq2,
+                     Tw, g.ids, g.ids2, g.kvrow, g.kvrow2, Tc, t, s);
+      std::swap(g.seq, g.seq2);
+      std::swap(g.ids, g.ids2);
+      std::swap(g.kvrow, g.kvrow2);
+    };
+    if (fused_step)  // (beam 0's finalists only: every source is beam 0 at t = 0)
+      fused(0, nullptr, 1, g.bprob);
+    else if (slab_decode())
       beam_step_topk_slab(g.logits, g.dstats, nullptr, 1, B, L.V, k, decode_logsm, g.cand_v, g.cand_i, g.bprob, g.bsrc,
                           g.btok, s);
     else
       beam_step_topk(g.logits, nullptr, 1, B, L.V, k, decode_logsm, g.cand_v, g.cand_i, g.bprob, g.bsrc, g.btok, s);
-    CAPGEN_HIP(hipMemsetAsync(g.bsrc, 0, sizeof(int32_t) * R, s));  // all beams descend from beam 0 at t = 0
+    if (!fused_step) CAPGEN_HIP(hipMemsetAsync(g.bsrc, 0, sizeof(int32_t) * R, s));  // all beams descend from beam 0
     // The K/V cache is never copied: row r writes its position-t K/V at [l][r][t] and reads
     // position j of its history from row kvrow[r][j] (the beam it descended from there); a
     // reorder moves only the ids / sequences and this [R][Tc] table
@@ -2138,9 +2151,14 @@ struct capgen_engine {
       std::swap(g.ids, g.ids2);
       std::swap(g.kvrow, g.kvrow2);
     };
-    reorder(0);
+    if (!fused_step) reorder(0);
     for (int t = 1; t < Tw - 1; ++t) {
       dec_step(R, B, N, t, g.cache, g.ids, false, s, g.kvrow);
+      if (fused_step) {
+        fused(t, g.bprob, k, g.bprob2);
+        std::swap(g.bprob, g.bprob2);
+        continue;
+      }
       if (slab_decode())
         beam_step_topk_slab(g.logits, g.dstats, g.bprob, k, B, L.V, k, decode_logsm, g.cand_v, g.cand_i, g.bprob2,
                             g.bsrc, g.btok, s);

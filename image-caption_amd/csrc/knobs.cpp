@@ -42,6 +42,7 @@ constexpr KnobDef kDefs[] = {
     {Knob::CeVec8, "CE_VEC8", 1, false},                    // ce_finish with 16-B accesses
     {Knob::BregDecode, "BREG_DECODE", 1, false},            // decode GEMMs on the register-B kernel
     {Knob::DecodeLnFold, "DECODE_LN_FOLD", 1, false},       // decode LayerNorms in the consumer GEMM (2: every site)
+    {Knob::FusedBeamStep, "FUSED_BEAM_STEP", 1, false},     // beam selection + reorder in one launch per step
     // scheduling modes swept by the hazard tests / data-parallel options
     {Knob::OverlapFront, "OVERLAP_FRONT", 1, false},  // decoder front beside the encoder
     {Knob::OverlapDec0, "OVERLAP_DEC0", 1, false},    // decoder block 0 half beside the encoder backward

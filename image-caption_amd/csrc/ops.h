@@ -120,6 +120,12 @@ void beam_step_topk(const float* logits, const float* prev, int k_in, int B, int
 bool slab_select_ok(int V);
 void slab_argmax(const float* logits, const float2* stats, int B, int V, int64_t* ids_out, int64_t ids_ld, int col,
                  int32_t* next_ids, int64_t next_ld, hipStream_t s);
+// the bf16 beam step of every image in one launch (slab selection + merge + the reorder of the sequences,
+// ids and K/V row table into the *_dst buffers, chosen token at column t + 1; ops.hip)
+void beam_slab_step(const float* logits, const float2* stats, const float* prev, int k_in, int B, int V, int k,
+                    int logsm, float* out_prob, int32_t* out_src, int32_t* out_tok, const int64_t* seq_src,
+                    int64_t* seq_dst, int Tw, const int32_t* ids_src, int32_t* ids_dst, const int32_t* kv_src,
+                    int32_t* kv_dst, int Tc, int t, hipStream_t s);
 void beam_step_topk_slab(const float* logits, const float2* stats, const float* prev, int k_in, int B, int V, int k,
                          int logsm, float* cand_v, int32_t* cand_i, float* out_prob, int32_t* out_src,
                          int32_t* out_tok, hipStream_t s);

@@ -1317,16 +1317,13 @@ void slab_argmax(const float* logits, const float2* stats, int B, int V, int64_t
   CAPGEN_HIP(hipGetLastError());
 }
 
+// one row's k best (value desc, index asc) from its slab stats: a wave per row, lane 0 leaves them in
+// (out_v, out_i)[0 .. k); chosen = this wave's KM-entry LDS scratch (row j = beam index)
 template <int KM>
-__global__ void __launch_bounds__(256) slab_row_topk_kernel(const float* __restrict__ logits,
-                                                            const float2* __restrict__ stats,
-                                                            const float* __restrict__ prev, int rows, int B, int V,
-                                                            int k, int logsm, float* __restrict__ cand_v,
-                                                            int* __restrict__ cand_i) {
-  __shared__ int chosen[4][KM];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = blockIdx.x * 4 + wave;
-  if (r >= rows) return;  // (whole waves; no workgroup barrier below)
-  const int S = (V + 15) / 16, j = r / B;
+__device__ __forceinline__ void slab_row_topk_wave(const float* __restrict__ logits, const float2* __restrict__ stats,
+                                                   const float* __restrict__ prev, int r, int j, int V, int k,
+                                                   int logsm, int* chosen, int lane, float* out_v, int* out_i) {
+  const int S = (V + 15) / 16;
   float mx[kSlabNS];
   const SlabRow rs = slab_row_stats(stats + (int64_t)r * S, S, lane, mx);
   // each lane's best KM slabs, sorted; then k wave rounds pick the row's k best slabs
@@ -1343,7 +1340,7 @@ __global__ void __launch_bounds__(256) slab_row_topk_kernel(const float* __restr
     float best = tv[0];
     int bidx = ti[0], bpos = lane;
     wave_best(best, bidx, bpos);
-    if (lane == 0) chosen[wave][sel] = bidx;  // (0x7fffffff when S < k: no such slab)
+    if (lane == 0) chosen[sel] = bidx;  // (0x7fffffff when S < k: no such slab)
     if (lane == bpos) {
 #pragma unroll
       for (int u = 0; u + 1 < KM; ++u) tv[u] = tv[u + 1], ti[u] = ti[u + 1];
@@ -1358,7 +1355,7 @@ __global__ void __launch_bounds__(256) slab_row_topk_kernel(const float* __restr
   for (int u = 0; u < KM; ++u) tv[u] = -INFINITY, ti[u] = 0x7fffffff;
   const float* x = logits + (int64_t)r * V;
   for (int e = lane; e < k * 16; e += 64) {
-    const int sl = chosen[wave][e >> 4];
+    const int sl = chosen[e >> 4];
     if (sl == 0x7fffffff) continue;
     const int c = sl * 16 + (e & 15);
     if (c >= V) continue;
@@ -1369,13 +1366,121 @@ __global__ void __launch_bounds__(256) slab_row_topk_kernel(const float* __restr
     float best = tv[0];
     int bidx = ti[0], bpos = lane;
     wave_best(best, bidx, bpos);
-    if (lane == 0) cand_v[(int64_t)r * k + sel] = best, cand_i[(int64_t)r * k + sel] = bidx;
+    if (lane == 0) out_v[sel] = best, out_i[sel] = bidx;
     if (lane == bpos) {
 #pragma unroll
       for (int u = 0; u + 1 < KM; ++u) tv[u] = tv[u + 1], ti[u] = ti[u + 1];
       tv[KM - 1] = -INFINITY, ti[KM - 1] = 0x7fffffff;
     }
   }
+}
+
+template <int KM>
+__global__ void __launch_bounds__(256) slab_row_topk_kernel(const float* __restrict__ logits,
+                                                            const float2* __restrict__ stats,
+                                                            const float* __restrict__ prev, int rows, int B, int V,
+                                                            int k, int logsm, float* __restrict__ cand_v,
+                                                            int* __restrict__ cand_i) {
+  __shared__ int chosen[4][KM];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = blockIdx.x * 4 + wave;
+  if (r >= rows) return;  // (whole waves; no workgroup barrier below)
+  slab_row_topk_wave<KM>(logits, stats, prev, r, r / B, V, k, logsm, chosen[wave], lane, cand_v + (int64_t)r * k,
+                         cand_i + (int64_t)r * k);
+}
+
+// The whole beam step of one image in ONE workgroup (round 6): wave j takes beam row j * B + i's k best
+// (slab_row_topk_wave) into LDS, wave 0 merges the k_in * k finalists exactly as beam_merge_kernel, and
+// every thread then moves the image's k new rows -- sequences and ids gathered from their source beams
+// with the chosen token at column t + 1, and the beam K/V row table (model.py:186-198) -- which took
+// four more launches (merge, two gathers, the row table) per token.
+template <int KM>
+__global__ void __launch_bounds__(1024) beam_slab_step_kernel(
+    const float* __restrict__ logits, const float2* __restrict__ stats, const float* __restrict__ prev, int k_in,
+    int B, int V, int k, int logsm, float* __restrict__ out_prob, int32_t* __restrict__ out_src,
+    int32_t* __restrict__ out_tok, const int64_t* __restrict__ seq_src, int64_t* __restrict__ seq_dst, int Tw,
+    const int32_t* __restrict__ ids_src, int32_t* __restrict__ ids_dst, const int32_t* __restrict__ kv_src,
+    int32_t* __restrict__ kv_dst, int Tc, int t) {
+  __shared__ int chosen[16][KM];
+  __shared__ float cv[256];
+  __shared__ int ci[256];
+  __shared__ int bsrc[16], btok[16];
+  const int i = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (wave < k_in)
+    slab_row_topk_wave<KM>(logits, stats, prev, wave * B + i, wave, V, k, logsm, chosen[wave], lane, cv + wave * k,
+                           ci + wave * k);
+  __syncthreads();
+  if (wave == 0) {  // beam_merge_kernel over the LDS finalists (entry e = row e / k, rank e % k)
+    const int n = k_in * k;
+    float v[4];
+    int c[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = lane + 64 * u;
+      const bool on = e < n;
+      v[u] = on ? cv[e] : -INFINITY;
+      c[u] = on ? ci[e] : 0x7fffffff;
+    }
+    for (int sel = 0; sel < k; ++sel) {
+      float best = -INFINITY;
+      int bidx = 0x7fffffff, bpos = -1;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (v[u] > best || (v[u] == best && c[u] < bidx)) best = v[u], bidx = c[u], bpos = lane + 64 * u;
+      wave_best(best, bidx, bpos);
+      if (lane == 0) {
+        out_prob[sel * B + i] = best;
+        out_src[sel * B + i] = bsrc[sel] = bidx / V;
+        out_tok[sel * B + i] = btok[sel] = bidx % V;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (bpos == lane + 64 * u) v[u] = -INFINITY, c[u] = 0x7fffffff;
+    }
+  }
+  __syncthreads();
+  // the image's k new rows r = j * B + i from their source rows bsrc[j] * B + i (double-buffered arrays)
+  for (int e = threadIdx.x; e < k * (Tw + 2 * Tc); e += blockDim.x) {
+    const int j = e / (Tw + 2 * Tc), q = e % (Tw + 2 * Tc);
+    const int64_t r = (int64_t)j * B + i, srow = (int64_t)bsrc[j] * B + i;
+    if (q < Tw) {
+      seq_dst[r * Tw + q] = q == t + 1 ? (int64_t)btok[j] : seq_src[srow * Tw + q];
+    } else if (q < Tw + Tc) {
+      const int cc = q - Tw;
+      ids_dst[r * Tc + cc] = cc == t + 1 ? btok[j] : ids_src[srow * Tc + cc];
+    } else {
+      const int cc = q - Tw - Tc;
+      kv_dst[r * Tc + cc] = cc <= t ? kv_src[srow * Tc + cc] : (cc == t + 1 ? (int32_t)r : 0);
+    }
+  }
+}
+
+void beam_slab_step(const float* logits, const float2* stats, const float* prev, int k_in, int B, int V, int k,
+                    int logsm, float* out_prob, int32_t* out_src, int32_t* out_tok, const int64_t* seq_src,
+                    int64_t* seq_dst, int Tw, const int32_t* ids_src, int32_t* ids_dst, const int32_t* kv_src,
+                    int32_t* kv_dst, int Tc, int t, hipStream_t s) {
+  require(k >= 1 && k <= 16 && k_in >= 1 && k_in <= 16 && k_in * k <= 256, "beam_slab_step: k, k_in in [1, 16]");
+  require(slab_select_ok(V) && t + 1 < Tw && t + 1 < Tc, "beam_slab_step: V in [1, 16384], t + 1 < width");
+  if (hz::active()) {
+    using namespace hz;
+    const int R = k * B, S = (V + 15) / 16;
+    op(s, "beam_slab_step", {rd(logits, (int64_t)k_in * B * V * 4), rd(stats, (int64_t)k_in * B * S * 8),
+                             rd(prev, prev ? (int64_t)k_in * B * 4 : 0), wr(out_prob, (int64_t)k * B * 4),
+                             wr(out_src, (int64_t)k * B * 4), wr(out_tok, (int64_t)k * B * 4),
+                             rd(seq_src, (int64_t)R * Tw * 8), wr(seq_dst, (int64_t)R * Tw * 8),
+                             rd(ids_src, (int64_t)R * Tc * 4), wr(ids_dst, (int64_t)R * Tc * 4),
+                             rd(kv_src, (int64_t)R * Tc * 4), wr(kv_dst, (int64_t)R * Tc * 4)});
+  }
+  const int nt = 64 * k_in;
+  auto go = [&](auto km) {
+    beam_slab_step_kernel<decltype(km)::value><<<B, nt, 0, s>>>(logits, stats, prev, k_in, B, V, k, logsm, out_prob,
+                                                                out_src, out_tok, seq_src, seq_dst, Tw, ids_src,
+                                                                ids_dst, kv_src, kv_dst, Tc, t);
+  };
+  if (k <= 4) go(std::integral_constant<int, 4>{});
+  else if (k == 5) go(std::integral_constant<int, 5>{});
+  else if (k <= 8) go(std::integral_constant<int, 8>{});
+  else go(std::integral_constant<int, 16>{});
+  CAPGEN_HIP(hipGetLastError());
 }
 
 void beam_step_topk_slab(const float* logits, const float2* stats, const float* prev, int k_in, int B, int V, int k,

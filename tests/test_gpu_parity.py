@@ -825,6 +825,26 @@ def test_decode_tiles_follow_graph_replayed_steps():
     fresh.close()
 
 
+@pytest.mark.parametrize("logsm", [False, True])
+def test_fused_beam_step_bit_identical(set_knob, logsm):
+    """The bf16 beam step's selection and reorder in one launch per image (beam_slab_step, ops.hip:
+    row top-k from the slab stats, the per-image merge, the sequence / id / K-V row-table gathers)
+    against the separate launches (CAPGEN_FUSED_BEAM_STEP=0): C4-shape beam ids bit-identical, with
+    Softmax probabilities (Transformer) and LogSoftmax (PolicyNetwork, model_RL.py:182)."""
+    set_knob("FUSED_BEAM_STEP", 0)
+    _, cfg, sd, e0, f, p, c = _c2_setup(B=256, dtype="bf16", weights="fixture")
+    set_knob("FUSED_BEAM_STEP", 1)
+    _, _, _, e1, _, _, _ = _c2_setup(B=256, dtype="bf16", weights="fixture")
+    fd, pd = f.to(DEV).bfloat16(), p.to(DEV)
+    for e in (e0, e1):
+        e.set_training(False)
+        e.set_decode_log_softmax(logsm)
+    for k in (5, 3):
+        assert torch.equal(e0.beam(fd, pd, k), e1.beam(fd, pd, k)), k
+    e0.close()
+    e1.close()
+
+
 def test_breg_decode_tracks_ring_decode(set_knob):
     """bf16 C4-style decode with the decoder Linears on the register-B GEMM (CAPGEN_BREG_DECODE,
     default on) against the LDS-ring GEMM: the products differ only in summation order inside the
