@@ -307,49 +307,63 @@ void layernorm_bwd(const LnBwd& a_in, DType t, hipStream_t s) {
 template <typename TI, typename TO>
 __global__ void __launch_bounds__(256) pack_kernel(const TI* __restrict__ feats, const float* __restrict__ pos,
                                                    const int32_t* __restrict__ img_idx, int n_img, int N, int F, int P,
-                                                   int Kp, TO* __restrict__ out, uint8_t* __restrict__ valid,
+                                                   int Kp, int M, TO* __restrict__ out, uint8_t* __restrict__ valid,
                                                    uint64_t* seed_bump) {
-  constexpr int V = 16 / sizeof(TI);  // one 16-B load of features per step
-  __shared__ int nz;
-  const int m = blockIdx.x;
+  // one wave per row m = (b, n), four rows per workgroup (round 6: the row-per-workgroup form spent its
+  // time on a workgroup barrier pair and an LDS atomic per position element; the region flag is now a
+  // wave ballot).  Features: 16-B loads, every load of the row issued before its stores.
+  constexpr int V = 16 / sizeof(TI);
+  const int lane = threadIdx.x & 63, m = blockIdx.x * 4 + (threadIdx.x >> 6);
   // the step's dropout seed advance rides along: nothing in this launch reads the seed
-  if (seed_bump && m == 0 && threadIdx.x == 0) *seed_bump += 0x9E3779B97F4A7C15ull;
-  // row m = (b, n) of the batch; with img_idx the features / positions of image img_idx[b] are
-  // read straight from an HBM-resident store (dataset.py:12-18 + DataLoader collate, fused)
+  if (seed_bump && blockIdx.x == 0 && threadIdx.x == 0) *seed_bump += 0x9E3779B97F4A7C15ull;
+  if (m >= M) return;  // (whole waves; no workgroup barrier in this kernel)
+  // with img_idx the features / positions of image img_idx[b] are read straight from an HBM-resident
+  // store (dataset.py:12-18 + DataLoader collate, fused)
   int64_t src = m;
+  TO* o = out + (int64_t)m * Kp;
   if (img_idx) {
     const int img = img_idx[m / N];
     if (img < 0 || img >= n_img) {  // out-of-range image: an all-padding row, never an OOB read
-      for (int c = threadIdx.x; c < Kp; c += 256) out[(int64_t)m * Kp + c] = from_f<TO>(0.f);
-      if (threadIdx.x == 0) valid[m] = 0;
+      for (int c = lane; c < Kp; c += 64) o[c] = from_f<TO>(0.f);
+      if (lane == 0) valid[m] = 0;
       return;
     }
     src = (int64_t)img * N + m % N;
   }
-  if (threadIdx.x == 0) nz = 0;
-  __syncthreads();
   const TI* f = feats + src * F;
   const float* p = pos + src * P;
-  TO* o = out + (int64_t)m * Kp;
-  for (int c = threadIdx.x * V; c < F; c += 256 * V) {
-    typedef typename Vec16<TI>::type VT;
-    const VT v = *reinterpret_cast<const VT*>(f + c);
-    const TI* e = reinterpret_cast<const TI*>(&v);
-    float x[V];
+  typedef typename Vec16<TI>::type VT;
+  constexpr int U = 4;  // 16-B loads in flight per lane
+  for (int c0 = lane * V; c0 < F; c0 += 64 * V * U) {
+    VT v[U];
 #pragma unroll
-    for (int j = 0; j < V; ++j) x[j] = to_f(e[j]);
-    store_f<TO, V>(o + c, x);
+    for (int u = 0; u < U; ++u) {
+      const int c = c0 + u * 64 * V;
+      if (c < F) v[u] = *reinterpret_cast<const VT*>(f + c);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = c0 + u * 64 * V;
+      if (c >= F) break;
+      const TI* e = reinterpret_cast<const TI*>(&v[u]);
+      float x[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) x[j] = to_f(e[j]);
+      store_f<TO, V>(o + c, x);
+    }
   }
-  for (int c = F + threadIdx.x; c < Kp; c += 256) {
+  // positions, then zeros to Kp; a region is padding iff its position row is all zero (model.py:206)
+  bool nz = false;
+  for (int c = F + lane; c < Kp; c += 64) {
     float x = 0.f;
     if (c < F + P) {
       x = p[c - F];
-      if (x != 0.f) atomicOr(&nz, 1);
+      nz |= x != 0.f;
     }
     o[c] = from_f<TO>(x);
   }
-  __syncthreads();
-  if (threadIdx.x == 0) valid[m] = nz ? 1 : 0;
+  const bool any = __ballot(nz) != 0;
+  if (lane == 0) valid[m] = any ? 1 : 0;
 }
 
 void pack_encoder_input(const void* feats, DType ft, const float* pos, int M, int F, int P, int Kp, void* out,
@@ -364,15 +378,15 @@ void pack_encoder_input(const void* feats, DType ft, const float* pos, int M, in
     op(s, "pack", {rd(feats, src_rows * F * (int64_t)dsize(ft)), rd(pos, src_rows * P * 4), rd(img_idx, img_idx ? M / N * 4 : 0),
                    wr(out, (int64_t)M * Kp * dsize(ot)), wr(valid, M), wr(seed_bump, 8)});
   }
-  dim3 grid(M);
+  dim3 grid((M + 3) / 4);
   if (ft == DType::F32 && ot == DType::F32)
-    pack_kernel<float, float><<<grid, 256, 0, s>>>((const float*)feats, pos, img_idx, n_img, N, F, P, Kp, (float*)out, valid, seed_bump);
+    pack_kernel<float, float><<<grid, 256, 0, s>>>((const float*)feats, pos, img_idx, n_img, N, F, P, Kp, M, (float*)out, valid, seed_bump);
   else if (ft == DType::F32 && ot == DType::BF16)
-    pack_kernel<float, bf16><<<grid, 256, 0, s>>>((const float*)feats, pos, img_idx, n_img, N, F, P, Kp, (bf16*)out, valid, seed_bump);
+    pack_kernel<float, bf16><<<grid, 256, 0, s>>>((const float*)feats, pos, img_idx, n_img, N, F, P, Kp, M, (bf16*)out, valid, seed_bump);
   else if (ft == DType::BF16 && ot == DType::BF16)
-    pack_kernel<bf16, bf16><<<grid, 256, 0, s>>>((const bf16*)feats, pos, img_idx, n_img, N, F, P, Kp, (bf16*)out, valid, seed_bump);
+    pack_kernel<bf16, bf16><<<grid, 256, 0, s>>>((const bf16*)feats, pos, img_idx, n_img, N, F, P, Kp, M, (bf16*)out, valid, seed_bump);
   else
-    pack_kernel<bf16, float><<<grid, 256, 0, s>>>((const bf16*)feats, pos, img_idx, n_img, N, F, P, Kp, (float*)out, valid, seed_bump);
+    pack_kernel<bf16, float><<<grid, 256, 0, s>>>((const bf16*)feats, pos, img_idx, n_img, N, F, P, Kp, M, (float*)out, valid, seed_bump);
   CAPGEN_HIP(hipGetLastError());
 }
 
