@@ -27,6 +27,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1, help="untimed calls first (CAPGEN_GEN_GRAPH=1 captures on the 2nd)")
     ap.add_argument("--modes", default="beam5,greedy")
     args = ap.parse_args()
     cfg = preset("C2", dtype="bf16")
@@ -43,7 +44,8 @@ def main():
     for name, fn in runs.items():
         if name not in args.modes.split(","):
             continue
-        fn()
+        for _ in range(args.warmup):
+            fn()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.reps):
